@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark of the Voxmap shading path on MI355X (BASELINE.json metric).
+
+A step renders one full frame of the headline workload (C3: 3840x2160, the
+reference's v1 shading = primary visibility + sun march + AO + sky/clouds +
+glass, on the synthetic S-proc 1024x256x32 field, camera K1) from the
+HBM-resident field into an HBM-resident RGBA8 framebuffer.
+
+N > 1 GPUs (one process per GPU, torchrun): weak scaling — the frame grows
+with N (W = 3840*sqrt(N), H = 2160*sqrt(N), so N = 4 is C4's 7680x4320),
+64x64 screen tiles are dealt round-robin to ranks, each rank renders its tiles
+and rank 0 gathers them over RCCL (torch.distributed "nccl") and de-tiles; the
+gather is inside the timed step.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+TILE = 64
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--camera", default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 PMC (tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if args.gpus > 1 and world == 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        world = max(world, 1)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = presets.CONFIGS[args.config]
+    cam = args.camera or cfg["camera"]
+    scale = math.sqrt(world)
+    W = int(round(cfg["w"] * scale / 16)) * 16
+    H = int(round(cfg["h"] * scale / 16)) * 16
+    up = 3.0 if cfg["scene"] == "s_up3" else 1.0
+
+    grid = presets.scene_grid(cfg["scene"])
+    Z, Y, X = grid.shape
+    field = vx.field_build(grid)
+    noise = vx.noise_synth(0)
+    scene = vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                     noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=local)
+    frame = presets.camera_frame(cam, W, H, scale=up)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    tiles_x, tiles_y = -(-W // TILE), -(-H // TILE)
+    n_tiles = tiles_x * tiles_y
+    if world == 1:
+        out = torch.empty(H * W * 4, dtype=torch.uint8, device="cuda")
+
+        def step():
+            scene.render_device(frame, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+
+        st = scene.render_device(frame, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
+        stats = st.as_dict()
+    else:
+        per = -(-n_tiles // world)
+        mine = [t for t in range(rank, n_tiles, world)]
+        mine_padded = mine + [mine[-1]] * (per - len(mine))        # equal gather sizes
+        all_ids = []
+        for r in range(world):
+            ids_r = list(range(r, n_tiles, world))
+            all_ids += ids_r + [ids_r[-1]] * (per - len(ids_r))
+        buf = torch.empty(per * TILE * TILE * 4, dtype=torch.uint8, device="cuda")
+        gather = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+        frame_buf = torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+        cat = torch.empty(world * buf.numel(), dtype=torch.uint8, device="cuda") if rank == 0 else None
+
+        def step():
+            scene.render_tiles(frame, TILE, mine_padded, buf.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+            dist.gather(buf, gather_list=gather, dst=0)
+            if rank == 0:
+                torch.cat(gather, out=cat)
+                scene.detile(W, H, TILE, all_ids, cat.data_ptr(), frame_buf.data_ptr(), pixel_format=vx.PIXEL_RGBA8,
+                             stream=stream)
+
+        st = scene.render_tiles(frame, TILE, mine, buf.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream,
+                                stats=True)
+        keys = list(st.as_dict().keys())
+        vec = torch.tensor([float(st.as_dict()[k]) for k in keys], dtype=torch.float64, device="cuda")
+        kms = torch.tensor([st.kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(vec)
+        stats = {k: float(v) for k, v in zip(keys, vec.tolist())}
+        stats["kernel_ms"] = float(st.kernel_ms)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1) / args.steps
+    t_local = wall
+    if world > 1:
+        tt = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_local = float(tt.item())
+    ms_per_step = 1000.0 * t_local / args.steps
+
+    rays = stats["pixels"] + stats["shadow_rays"]              # rays actually marched per frame
+    value = rays * args.steps / t_local / 1e6                 # whole-job Mrays/s
+    result = None
+    if rank == 0:
+        per_launch_bytes = float(stats["alg_bytes"]) / world if world > 1 else float(stats["alg_bytes"])
+        kernel_ms = ev_ms if world == 1 else stats["kernel_ms"]
+        achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        if world == 1 and os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("config") == args.config and tj.get("camera") == cam:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result = {
+            "metric": f"Mrays/s at {cfg['w']}x{cfg['h']} full quality ({args.config}); fps; % HBM roofline",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic S-proc field (seed 1) in map.bin layout; synthetic noise texture (real map.blob is "
+                    "AES-encrypted, key not in repo)",
+            "config": {
+                "workload": f"{args.config}: {W}x{H} frame, reference v1 shading (primary visibility + sun march + "
+                            f"trilinear AO + sky/clouds + glass), field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, "
+                            "RGBA8 framebuffer in HBM",
+                "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
+                "tiles": {"size": TILE, "count": n_tiles, "assignment": "round-robin"} if world > 1 else None,
+                "fps": round(1000.0 / ms_per_step, 2),
+                "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
+                "shadow_rays": int(stats["shadow_rays"]),
+                "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / t_local / 1e6, 3),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_render (fused primary+shade+shadow march)",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": int(per_launch_bytes),
+                "avg_launch_ms": round(kernel_ms, 4),
+            },
+        }
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(field, scene, noise, frame, W, H, args.cpu_seconds)
+    scene.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def cpu_baseline(field, scene, noise, frame, W, H, target_s):
+    """The scalar oracle (oracle/, -O2 -fno-fast-math -ffp-contract=off, OpenMP
+    over rows) on a deterministic 1-in-k row sample of the same frame."""
+    import numpy as np
+
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    dev_field = scene.read_field()            # same bytes (A channel included) the GPU marched
+    o = oracle.Oracle(dev_field, noise)
+    out = np.empty((H, W, 4), np.float32)
+    k = 256
+    t0 = time.perf_counter()
+    _, st = o.render(frame.params, W, H, row0=k // 2, row_step=k, threads=threads, out=out)
+    probe = time.perf_counter() - t0
+    k = max(1, min(256, int(math.ceil(k * probe / target_s)))) if probe > 0 else 16
+    t0 = time.perf_counter()
+    _, st = o.render(frame.params, W, H, row0=k // 2, row_step=k, threads=threads, out=out)
+    dt = time.perf_counter() - t0
+    rays = st.pixels + st.shadow_rays
+    return {
+        "value": round(rays / dt / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"rows {k // 2}::{k} of the same {W}x{H} frame ({st.pixels} pixels, {rays} rays) in {dt:.2f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()

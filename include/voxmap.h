@@ -1,0 +1,164 @@
+/*
+ * voxmap.h — C ABI of the MI355X-native Voxmap shading path (libvoxmap_hip.so).
+ *
+ * The reference's boundary for this path is the WebGL2 program interface of
+ * P.renderer (src/web/render.js:94-132): uniforms u_quality, u_matrix,
+ * u_cellPos, u_fractPos, u_frame, u_time, u_sunDir (src/shaders/render.h:5-11),
+ * samplers u_noise / u_map (render.js:138-149, 194-206), and the RGBA8 canvas
+ * the fragment shader writes (render.frag:4, map.js:7).  Its caller is
+ * drawScene() (render.js:267-298).  Each entry point below names the
+ * reference interface it replaces.  Plain C types only: pointers, sizes, ints.
+ *
+ * Conventions: return 0 = OK, < 0 = VX_E* code; the message of the last error
+ * on the calling thread is vx_last_error().  A scene owns device memory on one
+ * GPU; vx_render* calls are stream-ordered and may run concurrently on
+ * different scenes.  No global mutable state besides the thread-local error.
+ */
+#ifndef VOXMAP_H
+#define VOXMAP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VX_ABI_VERSION 1
+
+/* error codes */
+#define VX_OK 0
+#define VX_EINVAL (-1)   /* bad argument */
+#define VX_EIO (-2)      /* file read failure */
+#define VX_EFORMAT (-3)  /* gzip stream corrupt / not gzip */
+#define VX_ECRYPTO (-4)  /* bad key, bad padding, AES failure */
+#define VX_ESIZE (-5)    /* decoded size != expected (X*Y*Z*4, noise w*h*4) */
+#define VX_EDEVICE (-6)  /* HIP runtime error */
+#define VX_ENOMEM (-7)
+
+/* field / asset container formats (render.js:52-58, utils.js:10-30) */
+#define VX_FORMAT_AUTO 0    /* by extension: .blob -> BLOB, .gz -> BIN_GZ, else BIN */
+#define VX_FORMAT_BIN 1     /* raw RGBA8 bytes */
+#define VX_FORMAT_BIN_GZ 2  /* gzip of raw (makefile:70-71) */
+#define VX_FORMAT_BLOB 3    /* AES-256-CBC(PKCS#7, fixed IV) of gzip (encrypt.js:12-46) */
+
+/* output pixel formats */
+#define VX_PIXEL_RGBA32F 0  /* 16 B/pixel, parity format */
+#define VX_PIXEL_RGBA8 1    /* 4 B/pixel, what the canvas holds (map.js:185 toDataURL) */
+
+/* feature flags (vx_frame_params.flags); 0 = the reference v1 shader */
+#define VX_FLAG_NO_SHADOW 0x1u   /* skip the sun march (render.frag:232-235) */
+#define VX_FLAG_NO_AO 0x2u       /* skip the trilinear AO sample (render.frag:223-225) */
+#define VX_FLAG_NO_CLOUDS 0x4u   /* sky without noise fetches (render.frag:181-203) */
+
+typedef struct vx_scene vx_scene;
+
+/* Replaces loadTextures()/loadEncryptedTextures() (render.js:134-245):
+ * where the field (u_map) and noise (u_noise) come from.  Exactly one of
+ * map_path / map_bytes is set; noise may be absent (then a deterministic
+ * synthetic noise texture of the same layout is generated). */
+typedef struct vx_scene_desc {
+    const char *map_path;
+    const void *map_bytes;
+    size_t map_size;
+    int map_format;             /* VX_FORMAT_* */
+    const char *key_jwk_k;      /* JWK "k" (base64url AES-256 key) for BLOB; may be NULL */
+    const char *noise_path;
+    const void *noise_bytes;
+    size_t noise_size;
+    int noise_format;           /* VX_FORMAT_* */
+    int noise_w, noise_h;       /* 0 -> 1024 x 1024 (render.js:141) */
+    int X, Y, Z;                /* 0 -> 1024, 256, 32 (render.h:14-16) */
+    int device;                 /* HIP device ordinal */
+    int dist_cap;               /* A-channel distance cap, 0 -> 32 */
+    uint32_t noise_seed;        /* seed of the synthetic noise when none is given */
+} vx_scene_desc;
+
+/* Replaces the per-frame uniforms set in drawScene() (render.js:287-295).
+ * u_matrix is carried as the primary-ray basis (vx_frame_from_matrix /
+ * vx_frame_from_orbit derive it); the view ray of pixel (px,py) of a w*h
+ * frame is d = fwd + nx*right + ny*up with nx = (2px+1)/w - 1,
+ * ny = 1 - (2py+1)/h (fp32, this operation order). */
+typedef struct vx_frame_params {
+    int quality;                /* u_quality: 0 = 2D mode (base colour), 1 = lit */
+    int frame;                  /* u_frame (unused by render.frag, render.h:9) */
+    float time;                 /* u_time = t % 1000 seconds (render.js:293) */
+    int cam_cell[3];            /* u_cellPos = floor(camera position) */
+    float cam_fract[3];         /* u_fractPos = fract(camera position) */
+    float sun_dir[3];           /* u_sunDir (map.js:399-402) */
+    float ray_fwd[3];
+    float ray_right[3];
+    float ray_up[3];
+    uint32_t flags;             /* VX_FLAG_* */
+    int max_shadow_steps;       /* MAX_STEPS (render.frag:12); <= 0 -> 2*Z */
+} vx_frame_params;
+
+/* Counters of the work one vx_render call did (algorithmic). */
+typedef struct vx_stats {
+    uint64_t pixels, sky_px, block_px, glass_px;
+    uint64_t primary_fetches;   /* field texels read by the primary march */
+    uint64_t shadow_rays, shadow_fetches;
+    uint64_t ao_samples, noise_px;
+    uint64_t primary_cap_hits;  /* must be 0 */
+    uint64_t alg_bytes;         /* 4*fetches + 32*ao + 80*sky + out bytes */
+    double kernel_ms;           /* HIP-event time of the render kernel(s) */
+} vx_stats;
+
+/* --- scene lifetime ------------------------------------------------------ */
+int vx_scene_create(const vx_scene_desc *desc, vx_scene **out);
+void vx_scene_destroy(vx_scene *scene);
+/* Copy the device-resident field (RGBA8, A = primary-march distance) back. */
+int vx_scene_read_field(vx_scene *scene, void *host_out, size_t cap);
+int vx_scene_dims(const vx_scene *scene, int dims[3]);
+
+/* --- rendering (replaces gl.drawArrays at render.js:297 + the shaders) --- */
+/* Render a full w*h frame.  out is RGBA32F or RGBA8, row-major, top row
+ * first.  out_on_device != 0: out is a device pointer on the scene's GPU and
+ * the call returns without synchronising (stream-ordered); otherwise out is
+ * host memory and the call synchronises.  stream: hipStream_t or NULL (the
+ * scene's own stream).  stats may be NULL (counting costs one extra pass). */
+int vx_render(vx_scene *scene, const vx_frame_params *p, int w, int h, int pixel_format,
+              void *out, int out_on_device, void *stream, vx_stats *stats);
+
+/* Render only the listed tile_size x tile_size tiles (tile t covers pixels
+ * [(t % tiles_x)*ts, ...) with tiles_x = ceil(w/ts)) into a compact,
+ * tile-major device buffer: tile k of the list occupies ts*ts pixels at
+ * offset k*ts*ts, row-major inside the tile.  Used for screen-space sharding
+ * across GPUs. */
+int vx_render_tiles(vx_scene *scene, const vx_frame_params *p, int w, int h, int tile_size,
+                    const int *tile_ids, int n_tiles, int pixel_format, void *out_device,
+                    void *stream, vx_stats *stats);
+
+/* Scatter a compact tile-major device buffer back into a w*h frame. */
+int vx_detile(vx_scene *scene, int w, int h, int tile_size, const int *tile_ids, int n_tiles,
+              int pixel_format, const void *tiles_device, void *frame_device, void *stream);
+
+/* --- host helpers (map.js / math.js / sdf.cpp / utils.js) ----------------- */
+/* map.js:373-391 orbit camera + math.js:37-42 projection (with its sqrt(aspect)
+ * quirk): fills cam_cell/cam_fract/ray_* of p.  fov 60, near 1. */
+int vx_frame_from_orbit(const double sbj[3], const double rot[3], int w, int h, vx_frame_params *p);
+/* Same from a column-major u_matrix (render.js:288) and camera position. */
+int vx_frame_from_matrix(const float u_matrix[16], const double cam_pos[3], vx_frame_params *p);
+/* map.js:399-402: hour -> sun direction. */
+void vx_sun_from_hour(double hour, float sun[3]);
+
+/* Decode a field/asset container to raw bytes (render.js:52-58). */
+int vx_decode(const void *in, size_t n, int format, const char *key_jwk_k,
+              void *out, size_t out_cap, size_t *out_size);
+/* AES-256-CBC encrypt with the reference's fixed IV (encrypt.js:12-46). */
+int vx_blob_encrypt(const void *in, size_t n, const char *key_jwk_k,
+                    void *out, size_t out_cap, size_t *out_size);
+
+/* map.bin from a palette-index grid (x fastest): sdf.cpp:405-470.
+ * rgba_out holds X*Y*Z*4 bytes; A is written 0 as sdf.cpp:469 does. */
+int vx_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int n_threads);
+
+/* Deterministic synthetic noise texture in noise.bin layout (noise.cpp:34-41). */
+int vx_noise_synth(uint32_t seed, int w, int h, uint8_t *rgba_out);
+
+const char *vx_last_error(void);
+int vx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

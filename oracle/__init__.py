@@ -1,0 +1,140 @@
+"""CPU ORACLE bindings — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this package, and only as the checker / the timed CPU baseline.  The product
+path (voxmap_amd, libvoxmap_hip.so) never touches it.
+
+Parity status: "parity unpinned" against reference outputs (the reference is
+browser GLSL with no tests or golden images); the oracle is
+pinned by hand-derived known-answer tests (tests/test_oracle_kat.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libvxo.so")
+
+
+class OScene(C.Structure):
+    _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
+                ("noise_w", C.c_int), ("noise_h", C.c_int)]
+
+
+class OStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("pixels", "sky_px", "block_px", "glass_px", "primary_fetches",
+                                          "shadow_rays", "shadow_fetches", "ao_samples", "noise_px",
+                                          "primary_cap_hits")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class OMarch(C.Structure):
+    _fields_ = [("cell", C.c_int * 3), ("fract", C.c_float * 3), ("normal", C.c_float * 3), ("min_dist", C.c_float),
+                ("step", C.c_int), ("fetches", C.c_int)]
+
+
+class OGbuf(C.Structure):
+    _fields_ = [("id", C.c_int), ("color", C.c_int), ("normal_idx", C.c_int), ("cell", C.c_int * 3),
+                ("fract", C.c_float * 3)]
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.vxo_render.argtypes = [C.POINTER(OScene), C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                 C.POINTER(OStats), C.c_int]
+        L.vxo_render.restype = None
+        L.vxo_march.argtypes = [C.POINTER(OScene), C.POINTER(C.c_int), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                C.c_int, C.POINTER(OMarch)]
+        L.vxo_primary.argtypes = [C.POINTER(OScene), C.c_void_p, C.POINTER(C.c_float), C.POINTER(OGbuf),
+                                  C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.vxo_primary.restype = C.c_int
+        L.vxo_shade.argtypes = [C.POINTER(OScene), C.c_void_p, C.POINTER(OGbuf), C.POINTER(C.c_float),
+                                C.POINTER(C.c_float), C.c_void_p]
+        L.vxo_pixel_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+        L.vxo_exp2.argtypes = [C.c_float]
+        L.vxo_exp2.restype = C.c_float
+        L.vxo_field_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.vxo_field_dist.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    """Scalar restatement of render.frag over one field + noise texture."""
+
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray):
+        self.field = np.ascontiguousarray(field_zyx4, np.uint8)
+        self.noise = np.ascontiguousarray(noise_hw4, np.uint8)
+        Z, Y, X, _ = self.field.shape
+        H, W, _ = self.noise.shape
+        self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H)
+
+    def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
+        """RGBA fp32 (h, w, 4); rows not in (row0::row_step) are NaN."""
+        if out is None:
+            out = np.full((h, w, 4), np.nan, np.float32)
+        st = OStats()
+        lib().vxo_render(C.byref(self.sc), C.addressof(params), w, h, row0, row_step, out.ctypes.data,
+                         C.byref(st), threads)
+        return out, st
+
+    def march(self, cell, fract, direction, max_steps=None):
+        m = OMarch()
+        lib().vxo_march(C.byref(self.sc), (C.c_int * 3)(*cell), (C.c_float * 3)(*fract),
+                        (C.c_float * 3)(*direction), int(max_steps if max_steps else 2 * self.sc.Z), C.byref(m))
+        return m
+
+    def primary(self, params, direction):
+        g = (OGbuf * 2)()
+        fetches = C.c_int()
+        cap = C.c_int()
+        n = lib().vxo_primary(C.byref(self.sc), C.addressof(params), (C.c_float * 3)(*direction), g,
+                              C.byref(fetches), C.byref(cap))
+        return n, [g[0], g[1]], fetches.value, cap.value
+
+    def shade(self, params, gbuf, prim_dir):
+        out = (C.c_float * 4)()
+        lib().vxo_shade(C.byref(self.sc), C.addressof(params), C.byref(gbuf), (C.c_float * 3)(*prim_dir), out, None)
+        return tuple(out)
+
+    def pixel_dir(self, params, w, h, px, py):
+        d = (C.c_float * 3)()
+        lib().vxo_pixel_dir(C.addressof(params), w, h, px, py, d)
+        return tuple(d)
+
+
+def field_build(color_zyx: np.ndarray) -> np.ndarray:
+    col = np.ascontiguousarray(color_zyx, np.uint8)
+    Z, Y, X = col.shape
+    out = np.empty((Z, Y, X, 4), np.uint8)
+    lib().vxo_field_build(col.ctypes.data, X, Y, Z, out.ctypes.data)
+    return out
+
+
+def field_dist(field_zyx4: np.ndarray, cap: int = 32) -> np.ndarray:
+    out = np.ascontiguousarray(field_zyx4, np.uint8).copy()
+    Z, Y, X, _ = out.shape
+    lib().vxo_field_dist(out.ctypes.data, X, Y, Z, cap)
+    return out
+
+
+def exp2(x: float) -> float:
+    return lib().vxo_exp2(float(x))

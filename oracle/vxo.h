@@ -1,0 +1,120 @@
+/*
+ * vxo.h — CPU ORACLE for the Voxmap shading path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This is a scalar C restatement of the reference's per-pixel path, written
+ * from reading the reference as text.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it, and only as the checker or the
+ * timed CPU baseline — never as part of the product path.
+ *
+ * PARITY STATUS: "parity unpinned" against reference outputs.  The reference
+ * is GLSL ES 3.00 running in a browser and has no tests, golden images or
+ * known-answer vectors; compiling/running the reference's
+ * C++ was refused by the environment, so it is read as text
+ * only.  The oracle is pinned instead by hand-derived known-answer tests
+ * (tests/test_oracle_kat.py: empty map, single block shadow footprint,
+ * closed-form sky, march() traces) and by the plaintext reference assets
+ * (res/noise.bin.gz checksums).
+ *
+ * Restated reference files (all under /root/reference):
+ *   src/shaders/render.frag:12-142   march(), texture helpers
+ *   src/shaders/render.frag:147-252  main() shading
+ *   src/shaders/render.h:2-24        constants, uniforms
+ *   src/shaders/render.vert:14-22    normal()/palette() tables
+ *   src/web/render.js:62,138-149,194-206  texel layout and sampler state
+ *   src/gen/sdf.cpp:405-470          field definition (see vxo_field.c)
+ */
+#ifndef VXO_H
+#define VXO_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int X, Y, Z;              /* field dims (render.h:14-16) */
+    const uint8_t *field;     /* RGBA8 X*Y*Z texels, x fastest (render.js:62) */
+    const uint8_t *noise;     /* RGBA8 noise texture (render.js:138-149) */
+    int noise_w, noise_h;
+} vxo_scene;
+
+/* Mirrors include/voxmap.h vx_frame_params field-for-field. */
+typedef struct {
+    int quality;              /* u_quality (render.h:5) */
+    int frame;                /* u_frame (unused by render.frag) */
+    float time;               /* u_time (render.h:10) */
+    int cam_cell[3];          /* u_cellPos */
+    float cam_fract[3];       /* u_fractPos */
+    float sun_dir[3];         /* u_sunDir */
+    float ray_fwd[3];         /* primary ray basis: d = fwd + nx*right + ny*up */
+    float ray_right[3];
+    float ray_up[3];
+    unsigned flags;
+    int max_shadow_steps;     /* MAX_STEPS = 2*Z (render.frag:12); <=0 -> 2*Z */
+} vxo_frame;
+
+typedef struct {
+    uint64_t pixels, sky_px, block_px, glass_px;
+    uint64_t primary_fetches;  /* texels read by the primary march */
+    uint64_t shadow_rays, shadow_fetches;
+    uint64_t ao_samples, noise_px;
+    uint64_t primary_cap_hits; /* primary marches that hit the iteration cap */
+} vxo_stats;
+
+/* march() result (render.frag:64-70) */
+typedef struct {
+    int cell[3];
+    float fract[3];
+    float normal[3];
+    float min_dist;
+    int step;
+    int fetches;
+} vxo_march_t;
+
+/* G-buffer record: what render.vert hands to render.frag (render.vert:24-31). */
+typedef struct {
+    int id;                   /* 0 block, 1 sky, 2 glass (sdf.cpp:337, :250-279) */
+    int color;                /* palette index (B channel) */
+    int normal_idx;           /* 0..5 (render.vert:14-17) */
+    int cell[3];              /* v_cellPos */
+    float fract[3];           /* v_fractPos */
+} vxo_gbuf;
+
+/* Literal march() (render.frag:75-142). */
+void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
+               const float dir[3], int max_steps, vxo_march_t *res);
+
+/* Primary visibility (replaces raster of vertex.bin).
+ * Returns the number of surface records written (0 = sky, 1 = opaque,
+ * 2 = glass in g[0] followed by what is behind it in g[1] (g[1].id may be 1). */
+int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float dir[3],
+                vxo_gbuf g[2], int *fetches, int *cap_hit);
+
+/* Shade one fragment (render.frag:147-252).  out_rgba[3] = alpha. */
+void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
+               const float prim_dir[3], float out_rgba[4], vxo_stats *st);
+
+/* Render rows r = row0, row0+row_step, ... of a w*h frame into out (RGBA fp32,
+ * row-major, top row first).  Rows not rendered are left untouched.
+ * Uses OpenMP over rows when compiled with it; n_threads<=0 -> default. */
+void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
+                int row0, int row_step, float *out, vxo_stats *st, int n_threads);
+
+/* Per-pixel ray direction for pixel (px,py) (float, fixed op order). */
+void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3]);
+
+/* Deterministic transcendental used by both oracle and kernel. */
+float vxo_exp2(float x);
+
+/* --- field (map.bin) definition, vxo_field.c ---------------------------- */
+/* Build the RGBA8 field from a palette-index grid (x fastest), restating
+ * sdf.cpp:405-470 literally (serial x->y->z order, clamped-index quirks). */
+void vxo_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba);
+/* Fill the A channel with the capped Chebyshev distance used by the primary
+ * march (A is written 0 by sdf.cpp:469 and unused by the GLSL). */
+void vxo_field_dist(uint8_t *rgba, int X, int Y, int Z, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

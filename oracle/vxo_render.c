@@ -1,0 +1,536 @@
+/*
+ * vxo_render.c — CPU ORACLE (test infrastructure only; see vxo.h header).
+ * "parity unpinned" against reference outputs (none exist); pinned by the
+ * hand-derived KATs in tests/test_oracle_kat.py.
+ *
+ * Scalar restatement of /root/reference/src/shaders/render.frag (+ render.h,
+ * render.vert) and of the primary-visibility rule the raster of vertex.bin
+ * implements (sdf.cpp:281-356 mesh + render.js:82-91 GL state).
+ *
+ * Numerical contract (shared with the HIP kernel):
+ *   - fp32 everywhere, IEEE +,-,*,/ and sqrt, no FMA contraction
+ *     (build with -O2 -fno-fast-math -ffp-contract=off);
+ *   - GLSL built-ins restated from the GLSL ES 3.00 definitions
+ *     (mix(x,y,a)=x*(1-a)+y*a, fract(x)=x-floor(x), min(x,y)=y<x?y:x, ...);
+ *   - exp2/exp use vxo_exp2 (one fixed polynomial, both sides);
+ *   - unorm8 texels decode to b/255 (then *255 == b exactly, checked);
+ *   - textures sampled at LOD 0 with fp32 weights, nested lerp x->y->z.
+ */
+#include "vxo.h"
+#include <math.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define GLASS_INDEX 21 /* palette slot of glass: render.vert:21, sdf.cpp:195,337 */
+
+/* ---------------- GLSL built-ins (GLSL ES 3.00 §8) ---------------- */
+static inline float g_min(float x, float y) { return y < x ? y : x; }
+static inline float g_max(float x, float y) { return x < y ? y : x; }
+static inline float g_clamp(float x, float a, float b) { return g_min(g_max(x, a), b); }
+static inline float g_fract(float x) { return x - floorf(x); }
+static inline float g_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+static inline float g_mix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+/* ivec(float): NaN -> 0 (gfx v_cvt_i32_f32 behaviour), saturate far outside
+ * any grid (such cells are out of bounds either way). */
+static inline int g_f2i(float x) {
+    if (x != x) return 0;
+    if (x > 16777216.0f) return 16777216;
+    if (x < -16777216.0f) return -16777216;
+    return (int)x;
+}
+
+/* exp2 on [0,1) by a fixed degree-9 Taylor polynomial in f, scaled by 2^n.
+ * GLSL leaves exp2's precision to the implementation (3+2|x| ulp); both the
+ * oracle and the kernel use this one definition so they agree bit for bit. */
+float vxo_exp2(float x) {
+    if (x != x) return x;
+    if (x >= 128.0f) return INFINITY;
+    if (x < -126.0f) return 0.0f;
+    float n = floorf(x);
+    float f = x - n;
+    float p = 1.0178086e-07f;
+    p = p * f + 1.3215487e-06f;
+    p = p * f + 1.5252734e-05f;
+    p = p * f + 1.5403530e-04f;
+    p = p * f + 1.3333558e-03f;
+    p = p * f + 9.6181291e-03f;
+    p = p * f + 5.5504109e-02f;
+    p = p * f + 2.4022651e-01f;
+    p = p * f + 6.9314718e-01f;
+    p = p * f + 1.0f;
+    return ldexpf(p, (int)n);
+}
+static inline float g_exp(float x) { return vxo_exp2(x * 1.44269504f); }
+
+/* ---------------- palette / normals (render.vert:14-22) ---------------- */
+static const float PALETTE[22][3] = {
+    {0.0f, 0.0f, 0.0f},
+    {0.0431373f, 0.0627451f, 0.0745098f},
+    {0.133333f, 0.490196f, 0.317647f},
+    {0.321569f, 0.262745f, 0.239216f},
+    {0.337255f, 0.423529f, 0.45098f},
+    {0.392157f, 0.211765f, 0.235294f},
+    {0.396078f, 0.403922f, 0.396078f},
+    {0.439216f, 0.486275f, 0.454902f},
+    {0.454902f, 0.403922f, 0.243137f},
+    {0.52549f, 0.65098f, 0.592157f},
+    {0.52549f, 0.756863f, 0.4f},
+    {0.568627f, 0.596078f, 0.623529f},
+    {0.647059f, 0.870588f, 0.894118f},
+    {0.666667f, 0.666667f, 0.666667f},
+    {0.741176f, 0.752941f, 0.729412f},
+    {0.768627f, 0.384314f, 0.262745f},
+    {0.780392f, 0.243137f, 0.227451f},
+    {0.854902f, 0.788235f, 0.65098f},
+    {0.964706f, 0.772549f, 0.333333f},
+    {0.984314f, 0.886275f, 0.317647f},
+    {1.0f, 1.0f, 1.0f},
+    {0.505882f, 0.780392f, 0.831373f},
+};
+static void palette(int p, float out[3]) {
+    if (p >= 0 && p < 22) { out[0] = PALETTE[p][0]; out[1] = PALETTE[p][1]; out[2] = PALETTE[p][2]; }
+    else { out[0] = out[1] = out[2] = 1.0f; } /* render.vert:21 trailing vec3(1) */
+}
+static void normal_vec(int n, float out[3]) {
+    out[0] = out[1] = out[2] = 0.0f;
+    if (n >= 0 && n < 6) out[n >> 1] = (n & 1) ? -1.0f : 1.0f;
+}
+
+/* ---------------- texture access ---------------- */
+static inline const uint8_t *texel(const vxo_scene *s, int x, int y, int z) {
+    /* render.js:62 project_xyzc: C*(X*(Y*z + y) + x) */
+    return s->field + 4 * ((size_t)x + (size_t)s->X * ((size_t)y + (size_t)s->Y * (size_t)z));
+}
+static inline float unorm(uint8_t b) { return (float)b / 255.0f; }
+
+/* tex(ivec3) (render.frag:37-39): texelFetch(...).rgb * 255. */
+static void tex_fetch(const vxo_scene *s, const int c[3], float rgb[3]) {
+    const uint8_t *t = texel(s, c[0], c[1], c[2]);
+    rgb[0] = unorm(t[0]) * 255.0f;
+    rgb[1] = unorm(t[1]) * 255.0f;
+    rgb[2] = unorm(t[2]) * 255.0f;
+}
+
+/* Linear sampling along one axis with CLAMP_TO_EDGE (render.js:200-203). */
+static inline void lin_axis(float coord, int size, int *i0, int *i1, float *a) {
+    float u = coord * (float)size - 0.5f;
+    float fl = floorf(u);
+    *a = u - fl;
+    int i = g_f2i(fl);
+    int j = i + 1;
+    *i0 = i < 0 ? 0 : (i > size - 1 ? size - 1 : i);
+    *i1 = j < 0 ? 0 : (j > size - 1 ? size - 1 : j);
+}
+
+/* tex(ivec3, vec3) (render.frag:40-42): texture(u_map, (vec3(c)+f)*Sf).rgb*255
+ * at LOD 0, channels R and G (the only ones sdf() uses). */
+static void tex_linear_rg(const vxo_scene *s, const int c[3], const float f[3], float rg[2]) {
+    const float Sf[3] = {1.0f / (float)s->X, 1.0f / (float)s->Y, 1.0f / (float)s->Z};
+    int i0[3], i1[3];
+    float a[3];
+    const int dims[3] = {s->X, s->Y, s->Z};
+    for (int k = 0; k < 3; k++) {
+        float coord = ((float)c[k] + f[k]) * Sf[k];
+        lin_axis(coord, dims[k], &i0[k], &i1[k], &a[k]);
+    }
+    for (int ch = 0; ch < 2; ch++) {
+        float v[2][2];
+        for (int kz = 0; kz < 2; kz++)
+            for (int ky = 0; ky < 2; ky++) {
+                int yy = ky ? i1[1] : i0[1], zz = kz ? i1[2] : i0[2];
+                float t0 = unorm(texel(s, i0[0], yy, zz)[ch]);
+                float t1 = unorm(texel(s, i1[0], yy, zz)[ch]);
+                v[kz][ky] = g_mix(t0, t1, a[0]);
+            }
+        float w0 = g_mix(v[0][0], v[0][1], a[1]);
+        float w1 = g_mix(v[1][0], v[1][1], a[1]);
+        rg[ch] = g_mix(w0, w1, a[2]) * 255.0f;
+    }
+}
+
+/* sdf(ivec3, vec3) (render.frag:55-58): min(r, g) of the filtered field. */
+static float sdf_lin(const vxo_scene *s, const int c[3], const float f[3]) {
+    float rg[2];
+    tex_linear_rg(s, c, f, rg);
+    return g_min(rg[0], rg[1]);
+}
+
+/* REPEAT wrap of an integer-valued float onto [0,n) (n a power of two). */
+static inline int wrap_idx(float fl, int n) {
+    float q = floorf(fl / (float)n);
+    return g_f2i(fl - q * (float)n) & (n - 1);
+}
+
+/* fbm(p) = noise(p).a = 1 - 2*texture(u_noise, p).a (render.frag:16-24),
+ * bilinear, REPEAT (render.js:141-146), LOD 0. */
+static float fbm(const vxo_scene *s, float px, float py) {
+    const int W = s->noise_w, H = s->noise_h;
+    float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
+    float fu = floorf(u), fv = floorf(v);
+    float a = u - fu, b = v - fv;
+    int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
+    int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+    float t00 = unorm(s->noise[4 * ((size_t)y0 * W + x0) + 3]);
+    float t10 = unorm(s->noise[4 * ((size_t)y0 * W + x1) + 3]);
+    float t01 = unorm(s->noise[4 * ((size_t)y1 * W + x0) + 3]);
+    float t11 = unorm(s->noise[4 * ((size_t)y1 * W + x1) + 3]);
+    float r0 = g_mix(t00, t10, a), r1 = g_mix(t01, t11, a);
+    float t = g_mix(r0, r1, b);
+    return 1.0f - 2.0f * t;
+}
+
+/* ---------------- march() (render.frag:75-142), literally ---------------- */
+void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
+               const float r[3], int max_steps, vxo_march_t *res) {
+    res->step = 0;
+    res->fetches = 0;
+    res->cell[0] = cell[0]; res->cell[1] = cell[1]; res->cell[2] = cell[2];
+    res->fract[0] = fract[0]; res->fract[1] = fract[1]; res->fract[2] = fract[2];
+    res->min_dist = (float)s->Z;                     /* :82 */
+    float m[3] = {0.0f, 0.0f, 0.0f};                 /* minAxisDir */
+    float safe = 1.0f;                               /* :86 */
+    const float dir = r[2] > 0.0f ? 1.0f : 0.0f;     /* :89 */
+    const float sg[3] = {g_sign(r[0]), g_sign(r[1]), g_sign(r[2])};
+    const float ar[3] = {fabsf(r[0]), fabsf(r[1]), fabsf(r[2])};
+    while (res->step < max_steps && safe != 0.0f) {  /* :92 */
+        float d[3], t[3];
+        for (int i = 0; i < 3; i++) d[i] = g_fract(-res->fract[i] * sg[i]) + 1e-4f;   /* :94 */
+        for (int i = 0; i < 3; i++) t[i] = d[i] / ar[i];                                /* :97 */
+        m[0] = t[0] <= g_min(t[1], t[2]) ? 1.0f : 0.0f;                                 /* :100-104 */
+        m[1] = t[1] <= g_min(t[2], t[0]) ? 1.0f : 0.0f;
+        m[2] = t[2] <= g_min(t[0], t[1]) ? 1.0f : 0.0f;
+        float v0 = m[0] * t[0], v1 = m[1] * t[1], v2 = m[2] * t[2];
+        float len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);                                 /* :105 */
+        for (int i = 0; i < 3; i++) res->fract[i] += r[i] * safe * len;                /* :118 */
+        for (int i = 0; i < 3; i++) {
+            float fl = floorf(res->fract[i]);
+            res->cell[i] += g_f2i(fl);                                                  /* :119 */
+            res->fract[i] = res->fract[i] - fl;                                         /* :120 */
+        }
+        if (res->cell[0] >= s->X || res->cell[1] >= s->Y || res->cell[2] >= s->Z ||
+            res->cell[0] < 0 || res->cell[1] < 0 || res->cell[2] < 0) {                 /* :123-126 */
+            res->step = max_steps;
+            break;
+        }
+        float rgb[3];
+        tex_fetch(s, res->cell, rgb);                                                   /* :128 */
+        res->fetches++;
+        safe = g_mix(rgb[0], rgb[1], 1.0f - dir);                                       /* :47-50 */
+        res->step++;                                                                    /* :135 */
+    }
+    for (int i = 0; i < 3; i++) res->normal[i] = -g_sign(r[i] * m[i]);                /* :139 */
+}
+
+/* ---------------- primary visibility ----------------
+ * The reference rasterises the greedy mesh of sdf.cpp:281-356.  That mesh has a
+ * face wherever two grid-adjacent cells differ in palette index (index 0 = air
+ * included, ccol() clamps at the grid edge so the grid boundary has no faces),
+ * oriented from the differing cell into the cell of the face's colour, and GL
+ * culls back faces (render.js:88-91).  So the visible opaque surface at a pixel
+ * is the first in-grid cell boundary along the view ray where the colour
+ * changes; the entered cell gives colour and id.  Glass (index 21) is drawn
+ * last and blended (render.js:84-86); the surface behind a glass entry is the
+ * next colour change, which is never glass, so one blend layer is exact.
+ *
+ * Traversal: ray/AABB entry, then a DDA over cells in camera-relative
+ * coordinates; in an air cell whose A byte holds Chebyshev distance D >= 3 the
+ * ray jumps (D-1.5)/|d|_inf, which cannot leave the air box around the cell.
+ */
+static inline int in_grid(const vxo_scene *s, const int a[3]) {
+    return a[0] >= 0 && a[1] >= 0 && a[2] >= 0 && a[0] < s->X && a[1] < s->Y && a[2] < s->Z;
+}
+
+int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
+                vxo_gbuf g[2], int *fetches, int *cap_hit) {
+    const int dims[3] = {s->X, s->Y, s->Z};
+    const float *o = f->cam_fract;
+    const int *cc = f->cam_cell;
+    float inv[3];
+    int stp[3];
+    float tlo = 0.0f, thi = INFINITY;
+    *fetches = 0;
+    *cap_hit = 0;
+    for (int i = 0; i < 3; i++) {
+        stp[i] = d[i] > 0.0f ? 1 : -1;
+        float lo = (float)(0 - cc[i]) - o[i];
+        float hi = (float)(dims[i] - cc[i]) - o[i];
+        if (d[i] != 0.0f) {
+            inv[i] = 1.0f / d[i];
+            float t0 = lo * inv[i], t1 = hi * inv[i];
+            if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
+            tlo = g_max(tlo, t0);
+            thi = g_min(thi, t1);
+        } else {
+            inv[i] = 0.0f;
+            if (!(lo <= 0.0f && 0.0f < hi)) return 0;
+        }
+    }
+    if (!(tlo < thi)) return 0;
+    float amax = g_max(g_max(fabsf(d[0]), fabsf(d[1])), fabsf(d[2]));
+    float inv_inf = 1.0f / amax;
+
+    int c[3];         /* camera-relative cell */
+    float tmax[3];
+    float tcur = tlo;
+    for (int i = 0; i < 3; i++) {
+        float p = o[i] + tcur * d[i];
+        int ci = g_f2i(floorf(p));
+        int lo = -cc[i], hi = dims[i] - cc[i] - 1;
+        c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
+    }
+    for (int i = 0; i < 3; i++)
+        tmax[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? 1 : 0)) - o[i]) * inv[i] : INFINITY;
+
+    int nrec = 0;
+    int abs_c[3] = {c[0] + cc[0], c[1] + cc[1], c[2] + cc[2]};
+    const uint8_t *tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
+    (*fetches)++;
+    int prev = tx[2];
+    int dist = tx[3];
+    const int cap = 4 * (dims[0] + dims[1] + dims[2]);
+    for (int iter = 0; iter < cap; iter++) {
+        if (prev == 0 && dist >= 3) {
+            /* Chebyshev skip inside the air box of the current cell */
+            tcur = tcur + ((float)dist - 1.5f) * inv_inf;
+            for (int i = 0; i < 3; i++) {
+                float p = o[i] + tcur * d[i];
+                c[i] = g_f2i(floorf(p));
+                tmax[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? 1 : 0)) - o[i]) * inv[i] : INFINITY;
+            }
+        } else {
+            int a = (tmax[0] <= tmax[1] && tmax[0] <= tmax[2]) ? 0 : (tmax[1] <= tmax[2] ? 1 : 2);
+            float tcross = tmax[a];
+            c[a] += stp[a];
+            tmax[a] = ((float)(c[a] + (stp[a] > 0 ? 1 : 0)) - o[a]) * inv[a];
+            tcur = tcross;
+            abs_c[0] = c[0] + cc[0]; abs_c[1] = c[1] + cc[1]; abs_c[2] = c[2] + cc[2];
+            if (!in_grid(s, abs_c)) return nrec;   /* left the grid: sky behind */
+            tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
+            (*fetches)++;
+            int col = tx[2];
+            dist = tx[3];
+            if (col != prev) {
+                vxo_gbuf *h = &g[nrec];
+                h->color = col;
+                h->id = col == GLASS_INDEX ? 2 : 0;
+                h->normal_idx = 2 * a + (stp[a] > 0 ? 1 : 0);
+                for (int i = 0; i < 3; i++) {
+                    if (i == a) {
+                        h->cell[i] = abs_c[i] + (stp[a] > 0 ? 0 : 1);
+                        h->fract[i] = 0.0f;
+                    } else {
+                        float p = o[i] + tcross * d[i];
+                        h->cell[i] = abs_c[i];
+                        h->fract[i] = p - (float)c[i];
+                    }
+                }
+                nrec++;
+                if (h->id != 2 || nrec == 2) return nrec;
+            }
+            prev = col;
+            continue;
+        }
+        abs_c[0] = c[0] + cc[0]; abs_c[1] = c[1] + cc[1]; abs_c[2] = c[2] + cc[2];
+        if (!in_grid(s, abs_c)) return nrec;
+        tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
+        (*fetches)++;
+        dist = tx[3];
+        /* prev stays 0: the skip cannot leave air */
+    }
+    *cap_hit = 1;
+    return nrec;
+}
+
+void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3]) {
+    float nx = (float)(2 * px + 1) / (float)w - 1.0f;
+    float ny = 1.0f - (float)(2 * py + 1) / (float)h;
+    for (int i = 0; i < 3; i++) d[i] = (f->ray_fwd[i] + nx * f->ray_right[i]) + ny * f->ray_up[i];
+}
+
+/* ---------------- main() (render.frag:147-252) ---------------- */
+static inline float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void normalize3(const float v[3], float out[3]) {
+    float l = sqrtf(dot3(v, v));
+    out[0] = v[0] / l; out[1] = v[1] / l; out[2] = v[2] / l;
+}
+
+void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
+               const float prim_dir[3], float o_color[4], vxo_stats *st) {
+    o_color[0] = 0.0f; o_color[1] = 0.0f; o_color[2] = 0.0f; o_color[3] = 1.0f;    /* :148 */
+    const int isSky = g->id == 1, isGlass = g->id == 2;                            /* :150-151 */
+    const float litCol[3] = {0.4f, 0.35f, 0.3f};                                   /* :153 */
+    float v_normal[3], v_color[3];
+    normal_vec(isSky ? 1 : g->normal_idx, v_normal);   /* sky quads carry normal 1 (sdf.cpp:249-278) */
+    palette(isSky ? 0 : g->color, v_color);
+    float rayDir[3];
+    if (isSky) {
+        normalize3(prim_dir, rayDir);   /* skybox modelled at infinity */
+    } else {
+        float v[3];
+        for (int i = 0; i < 3; i++)
+            v[i] = (float)(g->cell[i] - f->cam_cell[i]) + (g->fract[i] - f->cam_fract[i]);   /* :154 */
+        normalize3(v, rayDir);
+    }
+    float reflectDir[3];                                                           /* :155 reflect() */
+    {
+        float k = 2.0f * dot3(v_normal, rayDir);
+        for (int i = 0; i < 3; i++) reflectDir[i] = rayDir[i] - k * v_normal[i];
+    }
+    const float *sunDir = f->sun_dir;                                              /* :157 */
+    const float sunCol[3] = {1.4f, 1.0f, 0.5f};                                    /* :162 */
+    float sunFactor = g_max(0.0f, dot3(f->sun_dir, rayDir)) - 1.0f;                /* :163 */
+    float glow = vxo_exp2(8.0f * sunFactor);                                       /* :164 */
+    sunFactor = vxo_exp2(4000.0f * sunFactor) + 0.3f * glow;                       /* :165 */
+    float scatter = 1.0f - sqrtf(g_max(0.0f, sunDir[2]));                          /* :168 */
+    const float sp0[3] = {0.2f, 0.4f, 0.7f}, sp1[3] = {0.2f, 0.3f, 0.5f};
+    const float sc0[3] = {0.7f, 0.9f, 1.0f}, sc1[3] = {1.0f, 0.3f, 0.2f};
+    float spaceCol[3], scatterCol[3], atmCol[3], skyCol[3];
+    float rz = sqrtf(g_max(0.0f, reflectDir[2]));
+    for (int i = 0; i < 3; i++) {
+        spaceCol[i] = g_mix(sp0[i], sp1[i], scatter);                               /* :169 */
+        scatterCol[i] = g_mix(sc0[i], sc1[i], scatter);                             /* :170 */
+        atmCol[i] = g_mix(scatterCol[i], spaceCol[i], rz);                          /* :171 */
+        skyCol[i] = sunCol[i] * sunFactor + atmCol[i];                              /* :173 */
+        skyCol[i] = g_clamp(skyCol[i], 0.0f, 1.0f);                                 /* :176 */
+    }
+    if (isSky) {                                                                   /* :178 */
+        rayDir[2] = fabsf(rayDir[2]);                                               /* :179 */
+        if (f->flags & 0x4u) {   /* VX_FLAG_NO_CLOUDS: plain sky colour */
+            o_color[0] = skyCol[0]; o_color[1] = skyCol[1]; o_color[2] = skyCol[2];
+            return;
+        }
+        if (st) st->noise_px++;
+        float cloudCol[3];
+        float cloudTime = f->time * 4e-3f;                                          /* :183 */
+        float den = sqrtf(fabsf(rayDir[2]) + 0.03f);
+        float sx = rayDir[0] / den, sy = rayDir[1] / den;                           /* :184 */
+        sx = sx * 0.1f; sy = sy * 0.1f;                                             /* :185 */
+        float sl = sqrtf(sqrtf(sx * sx + sy * sy));
+        sx = sx * sl; sy = sy * sl;                                                 /* :186 */
+        float n0 = fbm(s, 2.0f * sx + cloudTime, 2.0f * sy + cloudTime);            /* :188 */
+        float n1 = fbm(s, 2.0f * sx - cloudTime, 2.0f * sy - cloudTime);            /* :189 */
+        sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);                               /* :187-190 */
+        sx = sx + 1e-4f * ((float)f->cam_cell[0] + f->cam_fract[0]);                /* :191 */
+        sy = sy + 1e-4f * ((float)f->cam_cell[1] + f->cam_fract[1]);
+        float cloudFactor = vxo_exp2(6.0f * (fbm(s, sx + 2.0f * cloudTime, sy + -9.0f * cloudTime) - 1.0f)); /* :192 */
+        float scf = sqrtf(cloudFactor);
+        for (int i = 0; i < 3; i++) cloudCol[i] = g_mix(sunCol[i], 0.8f, scf);     /* :193 */
+        float mountainPos = rayDir[0] / rayDir[1];                                  /* :195 */
+        float mountainHeight = 1.0f - fbm(s, 0.3f * mountainPos, 0.3f * mountainPos); /* :196 */
+        float mountainFactor = 2.0f - fbm(s, 2.0f * (mountainPos + rayDir[1]),
+                                          2.0f * (mountainPos + rayDir[2]));         /* :197 */
+        mountainHeight = mountainHeight / (g_exp(0.3f * mountainPos * mountainPos) * 6.0f); /* :198 */
+        if (mountainHeight > rayDir[2] && rayDir[1] > 0.0f && rayDir[2] > 0.0f) {   /* :199 */
+            const float mt[3] = {0.7f, 0.8f, 0.7f};
+            float a = mountainFactor * rayDir[2];
+            for (int i = 0; i < 3; i++) skyCol[i] = g_mix(skyCol[i], skyCol[i] * mt[i], a); /* :200 */
+        } else {
+            for (int i = 0; i < 3; i++) skyCol[i] = g_mix(skyCol[i], cloudCol[i], cloudFactor); /* :202 */
+        }
+        o_color[0] = skyCol[0]; o_color[1] = skyCol[1]; o_color[2] = skyCol[2];    /* :205 */
+        return;
+    }
+    /* block branch :207-251 */
+    const float *baseCol = v_color;                                                 /* :209 */
+    float an[3] = {fabsf(v_normal[0]), fabsf(v_normal[1]), fabsf(v_normal[2])};
+    const float M0[3] = {0.90f, 0.90f, 0.95f}, M1[3] = {0.95f, 0.95f, 1.00f}, M2[3] = {1.0f, 1.0f, 1.0f};
+    float normalCol[3];
+    for (int i = 0; i < 3; i++) normalCol[i] = (M0[i] * an[0] + M1[i] * an[1]) + M2[i] * an[2]; /* :211-215 */
+    if (v_normal[2] < 0.0f)                                                         /* :217 */
+        for (int i = 0; i < 3; i++) normalCol[i] = normalCol[i] * 0.8f;
+    float shadeCol[3];
+    for (int i = 0; i < 3; i++) shadeCol[i] = 0.7f * scatterCol[i];                 /* :220 */
+    float ambCol[3] = {1.0f, 1.0f, 1.0f};
+    if (!(f->flags & 0x2u)) {   /* VX_FLAG_NO_AO skips the sample */
+        if (st) st->ao_samples++;
+        int ac[3];
+        for (int i = 0; i < 3; i++) ac[i] = g->cell[i] + g_f2i(v_normal[i]);
+        float ambDist = sdf_lin(s, ac, g->fract);                                   /* :223 */
+        float ambFactor = g_min(1.0f - sqrtf(ambDist), 0.8f);                       /* :224 */
+        for (int i = 0; i < 3; i++) ambCol[i] = g_mix(1.0f, shadeCol[i], ambFactor); /* :225 */
+    }
+    float shadeFactor = f->sun_dir[2] < 0.0f ? 0.0f
+                        : sqrtf(g_max(0.0f, dot3(v_normal, f->sun_dir)));           /* :228-229 */
+    if (shadeFactor > 0.0f && !(f->flags & 0x1u)) {  /* :232; VX_FLAG_NO_SHADOW skips */
+        const int max_steps = f->max_shadow_steps > 0 ? f->max_shadow_steps : 2 * s->Z;
+        vxo_march_t sun;
+        vxo_march(s, g->cell, g->fract, sunDir, max_steps, &sun);                   /* :233 */
+        shadeFactor = shadeFactor * (sun.step == max_steps ? 1.0f : 0.0f);          /* :234 */
+        if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
+    }
+    float lightCol[3];
+    for (int i = 0; i < 3; i++) lightCol[i] = shadeCol[i] + litCol[i] * shadeFactor; /* :238 */
+    for (int i = 0; i < 3; i++) o_color[i] = baseCol[i];                            /* :241 */
+    if (f->quality > 0)                                                             /* :242-244 */
+        for (int i = 0; i < 3; i++) o_color[i] = o_color[i] * ((normalCol[i] * lightCol[i]) * ambCol[i]);
+    if (isGlass) {                                                                  /* :246-249 */
+        o_color[3] = 0.8f * vxo_exp2(dot3(rayDir, v_normal));
+        for (int i = 0; i < 3; i++) o_color[i] = o_color[i] * (0.2f * atmCol[i]);
+    }
+}
+
+/* One pixel: primary visibility, shading, glass blend (render.js:84-86
+ * SRC_ALPHA / ONE_MINUS_SRC_ALPHA over the surface behind). */
+static void render_pixel(const vxo_scene *s, const vxo_frame *f, int w, int h, int px, int py,
+                         float out[4], vxo_stats *st) {
+    float d[3];
+    vxo_pixel_dir(f, w, h, px, py, d);
+    vxo_gbuf g[2];
+    int fetches = 0, cap_hit = 0;
+    int n = vxo_primary(s, f, d, g, &fetches, &cap_hit);
+    if (st) { st->pixels++; st->primary_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
+    vxo_gbuf sky;
+    memset(&sky, 0, sizeof sky);
+    sky.id = 1;
+    sky.normal_idx = 1;
+    if (n == 0) {
+        if (st) st->sky_px++;
+        vxo_shade(s, f, &sky, d, out, st);
+    } else if (g[0].id != 2) {
+        if (st) st->block_px++;
+        vxo_shade(s, f, &g[0], d, out, st);
+    } else {
+        if (st) st->glass_px++;
+        float src[4], dst[4];
+        vxo_shade(s, f, &g[0], d, src, st);
+        vxo_shade(s, f, n == 2 ? &g[1] : &sky, d, dst, st);
+        float a = src[3];
+        for (int i = 0; i < 3; i++) out[i] = src[i] * a + dst[i] * (1.0f - a);
+    }
+    out[3] = 1.0f;
+}
+
+void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
+                int row0, int row_step, float *out, vxo_stats *st, int n_threads) {
+    if (row_step <= 0) row_step = 1;
+    int nrows = row0 < h ? (h - 1 - row0) / row_step + 1 : 0;
+    vxo_stats acc;
+    memset(&acc, 0, sizeof acc);
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel num_threads(n_threads)
+#endif
+    {
+        vxo_stats loc;
+        memset(&loc, 0, sizeof loc);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int k = 0; k < nrows; k++) {
+            int py = row0 + k * row_step;
+            for (int px = 0; px < w; px++)
+                render_pixel(s, f, w, h, px, py, out + 4 * ((size_t)py * w + px), &loc);
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            uint64_t *a = (uint64_t *)&acc, *b = (uint64_t *)&loc;
+            for (size_t i = 0; i < sizeof acc / sizeof(uint64_t); i++) a[i] += b[i];
+        }
+    }
+    if (st) *st = acc;
+    (void)n_threads;
+}

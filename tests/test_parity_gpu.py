@@ -1,0 +1,190 @@
+"""Parity of the HIP path (libvoxmap_hip.so on device 0) with the scalar oracle.
+
+Bar: bit-exact fp32 (DESIGN.md §5 numerical contract), identical work
+counters, identical A channel.  Sizes the oracle renders in seconds are
+compared on every pixel; the BASELINE sizes (C2 1920x1080, C3 3840x2160 on the
+1024x256x32 field) on a deterministic row subset (every k-th row, all columns)
+plus size-independent properties (RGBA8 == quantised RGBA32F, tiles == frame).
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(built):
+    if not _torch_gpu():
+        pytest.skip("no GPU visible")
+
+
+def _scene(vx, field, noise, dims):
+    X, Y, Z = dims
+    return vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                    noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0)
+
+
+def _diff(a, b):
+    return int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32)))
+
+
+def _compare(img, ref, rows=None):
+    if rows is not None:
+        img, ref = img[rows], ref[rows]
+    bad = _diff(img, ref)
+    if bad:
+        idx = np.argwhere(img.view(np.uint32) != ref.view(np.uint32))[:5]
+        rel = np.max(np.abs(img - ref) / np.maximum(np.abs(ref), 1e-6))
+        raise AssertionError(f"{bad} words differ (max rel {rel:.3g}); first at {idx.tolist()}")
+
+
+SMALL = [
+    # (scene seed, dims, sbj, rot)
+    (5, (96, 48, 16), (48.0, 24.0, 18.0), (1.1, 0.0, 0.6)),
+    (7, (96, 48, 16), (48.0, 24.0, 40.0), (1e-4, 0.0, -0.002)),
+    (11, (128, 64, 24), (-6.0, 32.0, 9.0), (1.45, 0.0, -math.pi / 2)),
+    (13, (128, 64, 24), (64.0, 32.0, 6.0), (1.3, 0.0, 2.4)),      # camera inside the grid
+]
+
+
+@pytest.mark.parametrize("seed,dims,sbj,rot", SMALL)
+def test_small_frames_bit_exact(seed, dims, sbj, rot, noise):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    grid = scenes.small_proc(seed, dims=dims, n_boxes=16, n_glass=6)
+    field = vx.field_build(grid)
+    fr = vx.make_frame(sbj, rot, 160, 96)
+    with _scene(vx, field, noise, dims) as sc:
+        dev_field = sc.read_field()
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, 160, 96)
+    _compare(img, ref)
+    g, o = st.as_dict(), ost.as_dict()
+    for k in o:
+        assert g[k] == o[k], (k, g[k], o[k])
+    assert st.primary_cap_hits == 0
+
+
+def test_field_distance_channel_matches_oracle(noise):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid("s_proc")
+    field = vx.field_build(grid)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        dev = sc.read_field()
+    assert np.array_equal(dev[..., :3], field[..., :3])
+    assert np.array_equal(dev, oracle.field_dist(field, 32))
+
+
+@pytest.fixture(scope="module")
+def full_scene(noise):
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_proc"))
+    sc = _scene(vx, field, noise, (1024, 256, 32))
+    yield sc, sc.read_field()
+    sc.close()
+
+
+@pytest.mark.parametrize("cfg,cam,step", [("C2", "K1", 9), ("C3", "K1", 37), ("C2", "K0", 11),
+                                          ("C2", "K2", 13)])
+def test_baseline_sizes_row_subset(full_scene, noise, cfg, cam, step):
+    import oracle
+    from voxmap_amd import presets
+    sc, dev_field = full_scene
+    c = presets.CONFIGS[cfg]
+    fr = presets.camera_frame(cam, c["w"], c["h"])
+    img, st = sc.render(fr, stats=True)
+    ref, _ = oracle.Oracle(dev_field, noise).render(fr.params, c["w"], c["h"], row0=step // 2, row_step=step,
+                                                    threads=16)
+    rows = np.arange(step // 2, c["h"], step)
+    _compare(img, ref, rows)
+    assert st.primary_cap_hits == 0
+    assert st.pixels == c["w"] * c["h"]
+
+
+def test_rgba8_is_quantised_rgba32f(full_scene):
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    sc, _ = full_scene
+    fr = presets.camera_frame("K1", 640, 360)
+    f32, _ = sc.render(fr)
+    u8, _ = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
+    expect = (np.clip(f32, 0, 1) * np.float32(255) + np.float32(0.5)).astype(np.uint8)
+    assert np.array_equal(u8, expect)
+
+
+def test_tiles_and_detile_equal_full_frame(full_scene):
+    import torch
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    sc, _ = full_scene
+    w, h, ts = 1000, 600, 64            # ragged: w, h not multiples of the tile
+    fr = presets.camera_frame("K1", w, h)
+    full, _ = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
+    tx, ty = -(-w // ts), -(-h // ts)
+    ids = list(range(tx * ty))[::-1]    # any order
+    tiles = torch.empty(len(ids) * ts * ts * 4, dtype=torch.uint8, device="cuda:0")
+    frame = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda:0")
+    sc.render_tiles(fr, ts, ids, tiles.data_ptr())
+    sc.detile(w, h, ts, ids, tiles.data_ptr(), frame.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().reshape(h, w, 4), full)
+
+
+@pytest.mark.parametrize("case", ["sun_axis_zero", "sun_below", "quality0", "no_shadow", "no_ao", "no_clouds",
+                                  "short_budget"])
+def test_edge_params(noise, case):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (96, 48, 16)
+    grid = scenes.small_proc(21, dims=dims, n_boxes=14, n_glass=4)
+    field = vx.field_build(grid)
+    kw = {}
+    if case == "sun_axis_zero":
+        kw["sun"] = (0.6, 0.0, 0.8)          # 0*inf = NaN path of march() (render.frag:94-105)
+    elif case == "sun_below":
+        kw["sun"] = (0.3, 0.2, -0.93)
+    elif case == "quality0":
+        kw["quality"] = 0
+    elif case == "no_shadow":
+        kw["flags"] = vx.FLAG_NO_SHADOW
+    elif case == "no_ao":
+        kw["flags"] = vx.FLAG_NO_AO
+    elif case == "no_clouds":
+        kw["flags"] = vx.FLAG_NO_CLOUDS
+    elif case == "short_budget":
+        kw["max_shadow_steps"] = 5
+    fr = vx.make_frame((48.0, 24.0, 18.0), (1.1, 0.0, 0.6), 128, 80, **kw)
+    with _scene(vx, field, noise, dims) as sc:
+        dev_field = sc.read_field()
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, 128, 80)
+    _compare(img, ref)
+    assert st.shadow_fetches == ost.shadow_fetches
+
+
+def test_campus_scene(noise):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets, scenes
+    field = vx.field_build(scenes.s_campus())
+    fr = presets.camera_frame("K1", 480, 270)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        dev_field = sc.read_field()
+        img, _ = sc.render(fr)
+    ref, _ = oracle.Oracle(dev_field, noise).render(fr.params, 480, 270, threads=16)
+    _compare(img, ref)

@@ -1,0 +1,120 @@
+"""ctypes mirror of include/voxmap.h (the C ABI of libvoxmap_hip.so).
+
+The shared library is the product; this module only declares its structs and
+signatures.  Loading fails loudly when the library is missing: there is no
+CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvoxmap_hip.so")
+
+VX_OK = 0
+VX_EINVAL, VX_EIO, VX_EFORMAT, VX_ECRYPTO, VX_ESIZE, VX_EDEVICE, VX_ENOMEM = -1, -2, -3, -4, -5, -6, -7
+ERROR_NAMES = {
+    VX_EINVAL: "VX_EINVAL", VX_EIO: "VX_EIO", VX_EFORMAT: "VX_EFORMAT", VX_ECRYPTO: "VX_ECRYPTO",
+    VX_ESIZE: "VX_ESIZE", VX_EDEVICE: "VX_EDEVICE", VX_ENOMEM: "VX_ENOMEM",
+}
+
+FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB = 0, 1, 2, 3
+PIXEL_RGBA32F, PIXEL_RGBA8 = 0, 1
+FLAG_NO_SHADOW, FLAG_NO_AO, FLAG_NO_CLOUDS = 0x1, 0x2, 0x4
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("map_path", C.c_char_p), ("map_bytes", C.c_void_p), ("map_size", C.c_size_t),
+        ("map_format", C.c_int), ("key_jwk_k", C.c_char_p),
+        ("noise_path", C.c_char_p), ("noise_bytes", C.c_void_p), ("noise_size", C.c_size_t),
+        ("noise_format", C.c_int), ("noise_w", C.c_int), ("noise_h", C.c_int),
+        ("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int),
+        ("device", C.c_int), ("dist_cap", C.c_int), ("noise_seed", C.c_uint32),
+    ]
+
+
+class FrameParams(C.Structure):
+    """vx_frame_params: the per-frame uniforms of drawScene (render.js:287-295)."""
+    _fields_ = [
+        ("quality", C.c_int), ("frame", C.c_int), ("time", C.c_float),
+        ("cam_cell", C.c_int * 3), ("cam_fract", C.c_float * 3), ("sun_dir", C.c_float * 3),
+        ("ray_fwd", C.c_float * 3), ("ray_right", C.c_float * 3), ("ray_up", C.c_float * 3),
+        ("flags", C.c_uint32), ("max_shadow_steps", C.c_int),
+    ]
+
+    def copy(self) -> "FrameParams":
+        out = FrameParams()
+        C.memmove(C.byref(out), C.byref(self), C.sizeof(FrameParams))
+        return out
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("pixels", C.c_uint64), ("sky_px", C.c_uint64), ("block_px", C.c_uint64), ("glass_px", C.c_uint64),
+        ("primary_fetches", C.c_uint64), ("shadow_rays", C.c_uint64), ("shadow_fetches", C.c_uint64),
+        ("ao_samples", C.c_uint64), ("noise_px", C.c_uint64), ("primary_cap_hits", C.c_uint64),
+        ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# (name, restype, argtypes) of every symbol include/voxmap.h declares
+SIGNATURES = [
+    ("vx_scene_create", C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_void_p)]),
+    ("vx_scene_destroy", None, [C.c_void_p]),
+    ("vx_scene_read_field", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("vx_scene_dims", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    ("vx_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
+                            C.c_void_p, C.c_int, C.c_void_p, C.POINTER(Stats)]),
+    ("vx_render_tiles", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
+                                  C.POINTER(C.c_int), C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                  C.POINTER(Stats)]),
+    ("vx_detile", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int,
+                            C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("vx_frame_from_orbit", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
+                                      C.POINTER(FrameParams)]),
+    ("vx_frame_from_matrix", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(FrameParams)]),
+    ("vx_sun_from_hour", None, [C.c_double, C.POINTER(C.c_float)]),
+    ("vx_decode", C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_char_p, C.c_void_p, C.c_size_t,
+                            C.POINTER(C.c_size_t)]),
+    ("vx_blob_encrypt", C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, C.c_void_p, C.c_size_t,
+                                  C.POINTER(C.c_size_t)]),
+    ("vx_field_build", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
+    ("vx_noise_synth", C.c_int, [C.c_uint32, C.c_int, C.c_int, C.c_void_p]),
+    ("vx_last_error", C.c_char_p, []),
+    ("vx_abi_version", C.c_int, []),
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libvoxmap_hip.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"voxmap_amd: HIP library not built ({LIB_PATH} missing); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` — there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class VoxmapError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def check(rc: int) -> None:
+    if rc != VX_OK:
+        raise VoxmapError(rc, lib().vx_last_error().decode(errors="replace"))

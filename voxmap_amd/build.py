@@ -1,0 +1,51 @@
+"""In-tree build of libvoxmap_hip.so for gfx950 (hipcc, no JIT cache).
+
+Flags that are part of the numerical contract:
+  -ffp-contract=off      no FMA contraction (HIP's default is fast-honor-pragmas)
+  (default) -fhip-fp32-correctly-rounded-divide-sqrt  IEEE fp32 / and sqrt
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libvoxmap_hip.so")
+SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_kernels.hip"]
+ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-Wall", f"--offload-arch={ARCH}"]
+LIBS = ["-lz", "-lcrypto", "-lpthread"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.sep not in cand or os.path.exists(cand)):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [
+        os.path.join(CSRC, "vx_internal.h"), os.path.join(HERE, "..", "include", "voxmap.h")]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-shared", "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES], *LIBS]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,448 @@
+// vx_api.cpp — the C ABI (include/voxmap.h) over the HIP kernels.
+//
+// Replaces the WebGL host of the reference (src/web/render.js): texture
+// upload (render.js:134-206) becomes vx_scene_create (field + noise resident
+// in HBM, A channel filled on the GPU), drawScene (render.js:267-298) becomes
+// vx_render / vx_render_tiles.  The camera/sun helpers restate map.js:349-402
+// and math.js:16-49 in double precision, as the JS computes them.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include "vx_internal.h"
+
+namespace vx {
+int decode_container(const unsigned char *in, size_t n, int format, const char *key,
+                     std::vector<unsigned char> &out, size_t expect);
+int format_from_path(const char *path);
+int encrypt_blob(const unsigned char *in, size_t n, const char *key, std::vector<unsigned char> &out);
+int field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba, int n_threads);
+int noise_synth(uint32_t seed, int w, int h, uint8_t *out);
+
+static thread_local std::string g_err;
+int set_error(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace vx
+
+using namespace vx;
+
+struct vx_scene {
+    int device = 0;
+    int X = 0, Y = 0, Z = 0;
+    int noise_w = 0, noise_h = 0;
+    uint32_t *d_field = nullptr;
+    uint32_t *d_noise = nullptr;
+    unsigned long long *d_stats = nullptr;
+    int *d_tiles = nullptr;
+    int tiles_cap = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+#define VX_HIP(call)                                                                                 \
+    do {                                                                                             \
+        hipError_t e_ = (call);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            return set_error(VX_EDEVICE, std::string(#call " failed: ") + hipGetErrorString(e_));     \
+    } while (0)
+
+static int read_file(const char *path, std::vector<unsigned char> &buf) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return set_error(VX_EIO, std::string("cannot open ") + path);
+    buf.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    if (f.bad()) return set_error(VX_EIO, std::string("read error on ") + path);
+    return VX_OK;
+}
+
+static int load_asset(const char *path, const void *bytes, size_t size, int format, const char *key,
+                      size_t expect, const char *what, std::vector<unsigned char> &out) {
+    std::vector<unsigned char> raw;
+    const unsigned char *src = static_cast<const unsigned char *>(bytes);
+    size_t n = size;
+    if (path) {
+        int rc = read_file(path, raw);
+        if (rc) return rc;
+        src = raw.data();
+        n = raw.size();
+        if (format == VX_FORMAT_AUTO) format = format_from_path(path);
+    } else if (format == VX_FORMAT_AUTO) {
+        // sniff: gzip magic, else raw if the size matches, else assume blob
+        format = (n >= 2 && src[0] == 0x1f && src[1] == 0x8b) ? VX_FORMAT_BIN_GZ
+                 : (n == expect)                               ? VX_FORMAT_BIN
+                                                               : VX_FORMAT_BLOB;
+    }
+    int rc = decode_container(src, n, format, key, out, expect);
+    if (rc) return set_error(rc, std::string(what) + ": " + vx_last_error());
+    if (out.size() != expect)
+        return set_error(VX_ESIZE, std::string(what) + ": decoded " + std::to_string(out.size()) +
+                                       " bytes, expected " + std::to_string(expect));
+    return VX_OK;
+}
+
+extern "C" {
+
+const char *vx_last_error(void) { return g_err.c_str(); }
+int vx_abi_version(void) { return VX_ABI_VERSION; }
+
+int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
+    if (!d || !out) return set_error(VX_EINVAL, "vx_scene_create: null argument");
+    *out = nullptr;
+    const int X = d->X ? d->X : 1024, Y = d->Y ? d->Y : 256, Z = d->Z ? d->Z : 32;
+    const int NW = d->noise_w ? d->noise_w : 1024, NH = d->noise_h ? d->noise_h : 1024;
+    if (X <= 0 || Y <= 0 || Z <= 0 || X > 65535 || Y > 65535 || Z > 255)
+        return set_error(VX_EINVAL, "vx_scene_create: dims out of range");
+    if ((NW & (NW - 1)) || (NH & (NH - 1))) return set_error(VX_EINVAL, "noise dims must be powers of two");
+    if (!!d->map_path == !!d->map_bytes) return set_error(VX_EINVAL, "set exactly one of map_path / map_bytes");
+    const int cap = d->dist_cap ? d->dist_cap : 32;
+    if (cap < 1 || cap > 255) return set_error(VX_EINVAL, "dist_cap must be in [1,255]");
+    const size_t field_bytes = (size_t)X * Y * Z * 4, noise_bytes = (size_t)NW * NH * 4;
+
+    std::vector<unsigned char> field, noise;
+    int rc = load_asset(d->map_path, d->map_bytes, d->map_size, d->map_format, d->key_jwk_k, field_bytes, "map",
+                        field);
+    if (rc) return rc;
+    if (d->noise_path || d->noise_bytes) {
+        rc = load_asset(d->noise_path, d->noise_bytes, d->noise_size, d->noise_format, d->key_jwk_k, noise_bytes,
+                        "noise", noise);
+        if (rc) return rc;
+    } else {
+        noise.resize(noise_bytes);
+        rc = noise_synth(d->noise_seed, NW, NH, noise.data());
+        if (rc) return rc;
+    }
+    VX_HIP(hipSetDevice(d->device));
+    vx_scene *s = new vx_scene();
+    s->device = d->device;
+    s->X = X; s->Y = Y; s->Z = Z;
+    s->noise_w = NW; s->noise_h = NH;
+    auto fail = [&](int code) { vx_scene_destroy(s); return code; };
+    hipError_t e;
+    uint8_t *ga = nullptr, *gb = nullptr;
+    if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
+        (e = hipMalloc(&s->d_field, field_bytes)) != hipSuccess ||
+        (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
+        (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT)) != hipSuccess ||
+        (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
+        (e = hipMemcpyAsync(s->d_field, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s->d_noise, noise.data(), noise_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) {
+        if (ga) (void)hipFree(ga);
+        if (gb) (void)hipFree(gb);
+        return fail(set_error(VX_EDEVICE, std::string("scene upload failed: ") + hipGetErrorString(e)));
+    }
+    // A channel: primary-march distance, computed in HBM
+    int lrc = launch_field_dist(s->d_field, X, Y, Z, cap, ga, gb, s->stream);
+    e = hipStreamSynchronize(s->stream);
+    (void)hipFree(ga);
+    (void)hipFree(gb);
+    if (lrc != 0 || e != hipSuccess)
+        return fail(set_error(VX_EDEVICE, std::string("field distance pass failed: ") +
+                                              hipGetErrorString(lrc ? (hipError_t)lrc : e)));
+    *out = s;
+    return VX_OK;
+}
+
+void vx_scene_destroy(vx_scene *s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->d_field) (void)hipFree(s->d_field);
+    if (s->d_noise) (void)hipFree(s->d_noise);
+    if (s->d_stats) (void)hipFree(s->d_stats);
+    if (s->d_tiles) (void)hipFree(s->d_tiles);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+int vx_scene_dims(const vx_scene *s, int dims[3]) {
+    if (!s || !dims) return set_error(VX_EINVAL, "vx_scene_dims: null argument");
+    dims[0] = s->X; dims[1] = s->Y; dims[2] = s->Z;
+    return VX_OK;
+}
+
+int vx_scene_read_field(vx_scene *s, void *host_out, size_t cap) {
+    if (!s || !host_out) return set_error(VX_EINVAL, "vx_scene_read_field: null argument");
+    const size_t n = (size_t)s->X * s->Y * s->Z * 4;
+    if (cap < n) return set_error(VX_EINVAL, "vx_scene_read_field: buffer too small");
+    VX_HIP(hipSetDevice(s->device));
+    VX_HIP(hipMemcpyAsync(host_out, s->d_field, n, hipMemcpyDeviceToHost, s->stream));
+    VX_HIP(hipStreamSynchronize(s->stream));
+    return VX_OK;
+}
+
+static int check_params(const vx_scene *s, const vx_frame_params *p, int w, int h, int fmt) {
+    if (!s || !p) return set_error(VX_EINVAL, "null scene/params");
+    if (w <= 0 || h <= 0 || w > 32768 || h > 32768) return set_error(VX_EINVAL, "frame size out of range");
+    if (fmt != VX_PIXEL_RGBA32F && fmt != VX_PIXEL_RGBA8) return set_error(VX_EINVAL, "unknown pixel format");
+    for (int i = 0; i < 3; i++)
+        if (!std::isfinite(p->cam_fract[i]) || !std::isfinite(p->ray_fwd[i]) || !std::isfinite(p->ray_right[i]) ||
+            !std::isfinite(p->ray_up[i]) || !std::isfinite(p->sun_dir[i]))
+            return set_error(VX_EINVAL, "non-finite frame parameter");
+    return VX_OK;
+}
+
+static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int out_bytes) {
+    st->pixels = v[ST_PIXELS];
+    st->sky_px = v[ST_SKY];
+    st->block_px = v[ST_BLOCK];
+    st->glass_px = v[ST_GLASS];
+    st->primary_fetches = v[ST_PRIM_FETCH];
+    st->shadow_rays = v[ST_SHADOW_RAYS];
+    st->shadow_fetches = v[ST_SHADOW_FETCH];
+    st->ao_samples = v[ST_AO];
+    st->noise_px = v[ST_NOISE_PX];
+    st->primary_cap_hits = v[ST_CAP_HITS];
+    // 4 B per field texel read, 32 B per trilinear AO, 80 B per
+    // clouded sky pixel (5 bilinear noise taps), plus the framebuffer store.
+    st->alg_bytes = 4ull * (st->primary_fetches + st->shadow_fetches) + 32ull * st->ao_samples +
+                    80ull * st->noise_px + (unsigned long long)out_bytes * st->pixels;
+    st->kernel_ms = ms;
+}
+
+static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts, const int *tile_ids, int n_tiles,
+                     int fmt, void *out_dev, void *stream, vx_stats *stats) {
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    KernelArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.field = s->d_field;
+    a.noise = s->d_noise;
+    a.X = s->X; a.Y = s->Y; a.Z = s->Z;
+    a.noise_w = s->noise_w; a.noise_h = s->noise_h;
+    a.w = w; a.h = h;
+    a.tile_size = ts;
+    a.tiles_x = ts ? (w + ts - 1) / ts : 0;
+    a.tile_ids = tile_ids;
+    a.n_tiles = n_tiles;
+    a.out = out_dev;
+    a.p = *p;
+    a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
+    if (stats) {
+        a.stats = s->d_stats;
+        VX_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(unsigned long long) * ST_COUNT, st));
+    }
+    VX_HIP(hipEventRecord(s->ev0, st));
+    int rc = launch_render(a, fmt, st);
+    if (rc) return set_error(VX_EDEVICE, std::string("render launch failed: ") + hipGetErrorString((hipError_t)rc));
+    VX_HIP(hipEventRecord(s->ev1, st));
+    if (stats) {
+        unsigned long long v[ST_COUNT];
+        VX_HIP(hipMemcpyAsync(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost, st));
+        VX_HIP(hipStreamSynchronize(st));
+        float ms = 0.0f;
+        VX_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        fill_stats(stats, v, ms, fmt == VX_PIXEL_RGBA32F ? 16 : 4);
+    }
+    return VX_OK;
+}
+
+int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void *out, int out_on_device,
+              void *stream, vx_stats *stats) {
+    int rc = check_params(s, p, w, h, fmt);
+    if (rc) return rc;
+    if (!out) return set_error(VX_EINVAL, "vx_render: null output");
+    VX_HIP(hipSetDevice(s->device));
+    const size_t bytes = (size_t)w * h * (fmt == VX_PIXEL_RGBA32F ? 16 : 4);
+    if (out_on_device) return do_render(s, p, w, h, 0, nullptr, 0, fmt, out, stream, stats);
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    void *d_out = nullptr;
+    VX_HIP(hipMallocAsync(&d_out, bytes, st));
+    rc = do_render(s, p, w, h, 0, nullptr, 0, fmt, d_out, st, stats);
+    if (rc == VX_OK) {
+        hipError_t e = hipMemcpyAsync(out, d_out, bytes, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = set_error(VX_EDEVICE, std::string("readback failed: ") + hipGetErrorString(e));
+    }
+    (void)hipFreeAsync(d_out, st);
+    (void)hipStreamSynchronize(st);
+    return rc;
+}
+
+int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts, const int *tile_ids, int n_tiles,
+                    int fmt, void *out_device, void *stream, vx_stats *stats) {
+    int rc = check_params(s, p, w, h, fmt);
+    if (rc) return rc;
+    if (ts <= 0 || ts % 16) return set_error(VX_EINVAL, "tile_size must be a positive multiple of 16");
+    if (!tile_ids || n_tiles <= 0 || !out_device) return set_error(VX_EINVAL, "vx_render_tiles: empty tile list");
+    const int tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
+    for (int i = 0; i < n_tiles; i++)
+        if (tile_ids[i] < 0 || tile_ids[i] >= tx * ty) return set_error(VX_EINVAL, "tile id out of range");
+    VX_HIP(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    if (n_tiles > s->tiles_cap) {
+        if (s->d_tiles) VX_HIP(hipFree(s->d_tiles));
+        s->d_tiles = nullptr;
+        VX_HIP(hipMalloc(&s->d_tiles, sizeof(int) * n_tiles));
+        s->tiles_cap = n_tiles;
+    }
+    VX_HIP(hipMemcpyAsync(s->d_tiles, tile_ids, sizeof(int) * n_tiles, hipMemcpyHostToDevice, st));
+    return do_render(s, p, w, h, ts, s->d_tiles, n_tiles, fmt, out_device, st, stats);
+}
+
+int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tiles, int fmt, const void *tiles_device,
+              void *frame_device, void *stream) {
+    if (!s || !tile_ids || !tiles_device || !frame_device || ts <= 0 || n_tiles <= 0)
+        return set_error(VX_EINVAL, "vx_detile: bad arguments");
+    VX_HIP(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    int *d_ids = nullptr;
+    VX_HIP(hipMallocAsync(&d_ids, sizeof(int) * n_tiles, st));
+    VX_HIP(hipMemcpyAsync(d_ids, tile_ids, sizeof(int) * n_tiles, hipMemcpyHostToDevice, st));
+    int rc = launch_detile(tiles_device, frame_device, w, h, ts, (w + ts - 1) / ts, d_ids, n_tiles, fmt, st);
+    (void)hipFreeAsync(d_ids, st);
+    VX_HIP(hipStreamSynchronize(st));
+    if (rc) return set_error(VX_EDEVICE, std::string("detile failed: ") + hipGetErrorString((hipError_t)rc));
+    return VX_OK;
+}
+
+// ---- camera / sun (map.js:349-402, math.js:16-49,106-178) ----------------
+static void mat_mul(const double a[16], const double b[16], double r[16]) {   // column-major a*b (math.js:51-102)
+    for (int c = 0; c < 4; c++)
+        for (int rr = 0; rr < 4; rr++) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; k++) acc += a[k * 4 + rr] * b[c * 4 + k];
+            r[c * 4 + rr] = acc;
+        }
+}
+static void rot_x(double t, double m[16]) {   // math.js:144-154
+    const double c = std::cos(t), s = std::sin(t);
+    const double v[16] = {1, 0, 0, 0, 0, c, s, 0, 0, -s, c, 0, 0, 0, 0, 1};
+    std::memcpy(m, v, sizeof v);
+}
+static void rot_z(double t, double m[16]) {   // math.js:168-178
+    const double c = std::cos(t), s = std::sin(t);
+    const double v[16] = {c, s, 0, 0, -s, c, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    std::memcpy(m, v, sizeof v);
+}
+static void translation(double x, double y, double z, double m[16]) {   // math.js:137-142
+    const double v[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, x, y, z, 1};
+    std::memcpy(m, v, sizeof v);
+}
+static void set_cam(const double pos[3], vx_frame_params *p) {
+    for (int i = 0; i < 3; i++) {
+        const double fl = std::floor(pos[i]);
+        p->cam_cell[i] = (int)fl;               // render.js:289 position.map(floor)
+        p->cam_fract[i] = (float)(pos[i] - fl); // render.js:290 position.map(fract)
+    }
+}
+
+int vx_frame_from_orbit(const double sbj[3], const double rot[3], int w, int h, vx_frame_params *p) {
+    if (!sbj || !rot || !p || w <= 0 || h <= 0) return set_error(VX_EINVAL, "vx_frame_from_orbit: bad arguments");
+    // map.js:373-380: orbit = T(sbj) Rz(rz) Rx(rx) T(0,0,R), R = sbj.z; pos = orbit * (0,0,0,1)
+    double T1[16], Rz[16], Rx[16], T2[16], m1[16], m2[16], orbit[16];
+    translation(sbj[0], sbj[1], sbj[2], T1);
+    rot_z(rot[2], Rz);
+    rot_x(rot[0], Rx);
+    translation(0, 0, sbj[2], T2);
+    mat_mul(T1, Rz, m1);
+    mat_mul(m1, Rx, m2);
+    mat_mul(m2, T2, orbit);
+    const double pos[3] = {orbit[12], orbit[13], orbit[14]};
+    set_cam(pos, p);
+    // map.js:382-391 + math.js:37-42: P = projection(f, aspect) with x scale f/sqrt(a),
+    // y scale f*sqrt(a); view = Rx(-rx) Rz(-rz) T(-pos).  Eye ray for NDC (nx, ny):
+    // (nx*sqrt(a)/f, ny/(f*sqrt(a)), -1); world = Rz(rz) Rx(rx) eye.
+    const double f = 1.0 / std::tan(60.0 * M_PI / 360.0);
+    const double sa = std::sqrt((double)w / (double)h);
+    double RzRx[16];
+    mat_mul(Rz, Rx, RzRx);
+    auto apply = [&](double ex, double ey, double ez, float out[3]) {
+        for (int r = 0; r < 3; r++) out[r] = (float)(RzRx[0 * 4 + r] * ex + RzRx[1 * 4 + r] * ey + RzRx[2 * 4 + r] * ez);
+    };
+    apply(0, 0, -1, p->ray_fwd);
+    apply(sa / f, 0, 0, p->ray_right);
+    apply(0, 1.0 / (f * sa), 0, p->ray_up);
+    return VX_OK;
+}
+
+int vx_frame_from_matrix(const float m[16], const double cam_pos[3], vx_frame_params *p) {
+    if (!m || !cam_pos || !p) return set_error(VX_EINVAL, "vx_frame_from_matrix: null argument");
+    // invert the column-major u_matrix (double Gauss-Jordan), unproject NDC
+    // points on the far side of the near plane, subtract the camera position.
+    double a[4][8];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            a[r][c] = m[c * 4 + r];
+            a[r][4 + c] = r == c ? 1.0 : 0.0;
+        }
+    for (int c = 0; c < 4; c++) {
+        int piv = c;
+        for (int r = c + 1; r < 4; r++)
+            if (std::fabs(a[r][c]) > std::fabs(a[piv][c])) piv = r;
+        if (std::fabs(a[piv][c]) < 1e-300) return set_error(VX_EINVAL, "u_matrix is singular");
+        for (int k = 0; k < 8; k++) std::swap(a[c][k], a[piv][k]);
+        const double d = a[c][c];
+        for (int k = 0; k < 8; k++) a[c][k] /= d;
+        for (int r = 0; r < 4; r++)
+            if (r != c) {
+                const double fct = a[r][c];
+                for (int k = 0; k < 8; k++) a[r][k] -= fct * a[c][k];
+            }
+    }
+    auto unproj = [&](double x, double y, double out[3]) {
+        double v[4];
+        for (int r = 0; r < 4; r++) v[r] = a[r][4] * x + a[r][5] * y + a[r][6] * 1.0 + a[r][7] * 1.0;
+        for (int r = 0; r < 3; r++) out[r] = v[r] / v[3] - cam_pos[r];
+    };
+    double c0[3], cx[3], cy[3];
+    unproj(0, 0, c0);
+    unproj(1, 0, cx);
+    unproj(0, 1, cy);
+    // scale so the forward component has unit length along the eye axis
+    const double len = std::sqrt(c0[0] * c0[0] + c0[1] * c0[1] + c0[2] * c0[2]);
+    if (!(len > 0)) return set_error(VX_EINVAL, "degenerate u_matrix");
+    for (int i = 0; i < 3; i++) {
+        p->ray_fwd[i] = (float)(c0[i] / len);
+        p->ray_right[i] = (float)((cx[i] - c0[i]) / len);
+        p->ray_up[i] = (float)((cy[i] - c0[i]) / len);
+    }
+    set_cam(cam_pos, p);
+    return VX_OK;
+}
+
+void vx_sun_from_hour(double hour, float sun[3]) {   // map.js:399-402
+    sun[0] = (float)(std::sin(hour) * std::sqrt(3.0 / 4.0));
+    sun[1] = (float)(std::sin(hour) * std::sqrt(1.0 / 4.0));
+    sun[2] = (float)std::fabs(std::cos(hour));
+}
+
+int vx_decode(const void *in, size_t n, int format, const char *key, void *out, size_t out_cap, size_t *out_size) {
+    if (!in || !out_size) return set_error(VX_EINVAL, "vx_decode: null argument");
+    std::vector<unsigned char> buf;
+    int rc = decode_container(static_cast<const unsigned char *>(in), n, format, key, buf, 0);
+    if (rc) return rc;
+    *out_size = buf.size();
+    if (!out) return VX_OK;   // size query
+    if (out_cap < buf.size()) return set_error(VX_EINVAL, "vx_decode: output buffer too small");
+    std::memcpy(out, buf.data(), buf.size());
+    return VX_OK;
+}
+
+int vx_blob_encrypt(const void *in, size_t n, const char *key, void *out, size_t out_cap, size_t *out_size) {
+    if (!in || !out_size) return set_error(VX_EINVAL, "vx_blob_encrypt: null argument");
+    std::vector<unsigned char> buf;
+    int rc = encrypt_blob(static_cast<const unsigned char *>(in), n, key, buf);
+    if (rc) return rc;
+    *out_size = buf.size();
+    if (!out) return VX_OK;   // size query
+    if (out_cap < buf.size()) return set_error(VX_EINVAL, "vx_blob_encrypt: output buffer too small");
+    std::memcpy(out, buf.data(), buf.size());
+    return VX_OK;
+}
+
+int vx_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int n_threads) {
+    return field_build(color, X, Y, Z, rgba_out, n_threads);
+}
+
+int vx_noise_synth(uint32_t seed, int w, int h, uint8_t *rgba_out) { return noise_synth(seed, w, h, rgba_out); }
+
+}  // extern "C"

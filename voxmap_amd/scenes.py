@@ -1,0 +1,104 @@
+"""Synthetic scenes in the reference's map.bin format.
+
+The real field (res/map.blob) is AES-encrypted with a key that is not in the
+reference repository (src/web/ui.js:47,169-179), so benchmarks and parity
+tests run on synthetic palette-index grids with the same layout, turned into
+map.bin texels by ``vx_field_build`` (the sdf.cpp:405-470 restatement).
+
+Grids are (Z, Y, X) uint8 palette indices, x fastest in memory like map.bin
+(render.js:62).  Index 0 = air, 1..20 = opaque palette colours, 21 = glass
+(render.vert:21, sdf.cpp:195,337).
+"""
+from __future__ import annotations
+
+import gzip
+import os
+
+import numpy as np
+
+GLASS = 21
+_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def s_proc(seed: int = 1, dims=(1024, 256, 32), n_boxes: int = 400, n_glass: int = 30) -> np.ndarray:
+    """S-proc: ground, ~400 boxes (w 4-40, h 2-28, palette 1-20), ~5% overhang
+    slabs, 30 glass panes.  Deterministic in ``seed``."""
+    X, Y, Z = dims
+    rng = np.random.default_rng(seed)
+    g = np.zeros((Z, Y, X), np.uint8)
+    g[0] = 2                                   # grass ground at z = 0
+    # a few roads / courtyards on the ground plane
+    for _ in range(max(1, X // 64)):
+        if rng.random() < 0.5:
+            y0 = int(rng.integers(0, Y - 8)); g[0, y0:y0 + int(rng.integers(3, 8)), :] = 13
+        else:
+            x0 = int(rng.integers(0, X - 8)); g[0, :, x0:x0 + int(rng.integers(3, 8))] = 13
+    zmax = Z - 1
+    for _ in range(n_boxes):
+        w = int(rng.integers(4, 41)); d = int(rng.integers(4, 41))
+        hgt = int(rng.integers(2, min(29, zmax) + 1))
+        x0 = int(rng.integers(0, max(1, X - w))); y0 = int(rng.integers(0, max(1, Y - d)))
+        col = int(rng.integers(1, 21))
+        if rng.random() < 0.05:                # overhang slab: floating roof with air beneath
+            z0 = int(rng.integers(3, max(4, zmax - 3)))
+            t = int(rng.integers(1, 4))
+            g[z0:min(Z, z0 + t), y0:y0 + d, x0:x0 + w] = col
+            # one supporting pillar so it reads as a building
+            g[1:z0, y0:y0 + 2, x0:x0 + 2] = col
+        else:
+            g[1:1 + hgt, y0:y0 + d, x0:x0 + w] = col
+    for _ in range(n_glass):                   # glass panes, 1 voxel thick
+        L = int(rng.integers(6, 30)); hgt = int(rng.integers(3, min(20, zmax)))
+        x0 = int(rng.integers(0, X - L)); y0 = int(rng.integers(0, Y - L))
+        if rng.random() < 0.5:
+            g[1:1 + hgt, y0, x0:x0 + L] = GLASS
+        else:
+            g[1:1 + hgt, y0:y0 + L, x0] = GLASS
+    return g
+
+
+# colour -> storey height for the campus extrusion (deterministic, arbitrary:
+# the plaintext vertex2d.bin.gz carries top colours but no heights, sdf.cpp:156)
+_CAMPUS_HEIGHT = np.array([0, 1, 1, 6, 9, 12, 8, 7, 5, 1, 1, 10, 14, 4, 3, 11, 13, 6, 9, 16, 2, 8], np.int32)
+
+
+def campus_footprint() -> np.ndarray:
+    """(Y, X) top-colour map rasterised from the reference's plaintext
+    res/vertex2d.bin.gz by tools/make_campus_footprint.py."""
+    path = os.path.join(_DATA, "campus_footprint.npy.gz")
+    with gzip.open(path, "rb") as f:
+        return np.load(f, allow_pickle=False)
+
+
+def s_campus(dims=(1024, 256, 32)) -> np.ndarray:
+    """S-campus: the real campus footprint extruded by a fixed colour->height table."""
+    X, Y, Z = dims
+    fp = campus_footprint()
+    assert fp.shape == (Y, X), fp.shape
+    g = np.zeros((Z, Y, X), np.uint8)
+    g[0] = np.where(fp > 0, fp, 2).astype(np.uint8)
+    hgt = _CAMPUS_HEIGHT[np.minimum(fp, 21)]
+    hgt = np.minimum(hgt, Z - 1)
+    for z in range(1, Z):
+        m = hgt >= z
+        g[z][m] = fp[m]
+    return g
+
+
+def upsample3(g: np.ndarray, k: int = 3) -> np.ndarray:
+    """S-up3: nearest k-fold upsample (C5's 3072x768x96 field)."""
+    return np.repeat(np.repeat(np.repeat(g, k, axis=0), k, axis=1), k, axis=2)
+
+
+def single_block(dims=(64, 32, 16), at=(20, 12, 1), color=5) -> np.ndarray:
+    X, Y, Z = dims
+    g = np.zeros((Z, Y, X), np.uint8)
+    g[0] = 2
+    x, y, z = at
+    g[z, y, x] = color
+    return g
+
+
+def small_proc(seed: int, dims=(96, 48, 16), n_boxes=12, n_glass=3) -> np.ndarray:
+    """A small S-proc-like scene that the scalar oracle renders in seconds."""
+    return s_proc(seed, dims, n_boxes=n_boxes, n_glass=n_glass)
