@@ -100,6 +100,14 @@ def lib() -> C.CDLL:
             raise RuntimeError(
                 f"voxmap_amd: HIP library not built ({LIB_PATH} missing); run "
                 "`python -c 'import __graft_entry__ as g; g.build()'` — there is no CPU fallback")
+        # One HIP runtime per process: torch (the device-memory / stream /
+        # RCCL plumbing) bundles its own libamdhip64 under a different file
+        # name; loading torch first makes libvoxmap_hip.so bind to that same
+        # runtime (same SONAME) so device pointers and streams are shared.
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch-less hosts use /opt/rocm's runtime
+            pass
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)
