@@ -93,31 +93,19 @@ def main():
         st = scene.render_device(frame, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
         stats = st.as_dict()
     else:
-        per = -(-n_tiles // world)
-        mine = [t for t in range(rank, n_tiles, world)]
-        mine_padded = mine + [mine[-1]] * (per - len(mine))        # equal gather sizes
-        all_ids = []
-        for r in range(world):
-            ids_r = list(range(r, n_tiles, world))
-            all_ids += ids_r + [ids_r[-1]] * (per - len(ids_r))
-        buf = torch.empty(per * TILE * TILE * 4, dtype=torch.uint8, device="cuda")
-        gather = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-        frame_buf = torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
-        cat = torch.empty(world * buf.numel(), dtype=torch.uint8, device="cuda") if rank == 0 else None
-
-        def step():
-            scene.render_tiles(frame, TILE, mine_padded, buf.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
-            dist.gather(buf, gather_list=gather, dst=0)
-            if rank == 0:
-                torch.cat(gather, out=cat)
-                scene.detile(W, H, TILE, all_ids, cat.data_ptr(), frame_buf.data_ptr(), pixel_format=vx.PIXEL_RGBA8,
-                             stream=stream)
-
-        st = scene.render_tiles(frame, TILE, mine, buf.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream,
-                                stats=True)
-        keys = list(st.as_dict().keys())
+        from voxmap_amd.dist import ShardedFrame, TileLayout
+        layout = TileLayout(W, H, TILE)
+        sharded = ShardedFrame(
+            dist, layout, 4, torch.uint8, "cuda",
+            render_tiles=lambda ids, buf: scene.render_tiles(frame, TILE, ids, buf.data_ptr(),
+                                                             pixel_format=vx.PIXEL_RGBA8, stream=stream),
+            detile=lambda ids, cat, fr: scene.detile(W, H, TILE, ids, cat.data_ptr(), fr.data_ptr(),
+                                                     pixel_format=vx.PIXEL_RGBA8, stream=stream))
+        step = sharded.step
+        st = scene.render_tiles(frame, TILE, layout.rank_tiles(world, rank), sharded.buf.data_ptr(),
+                                pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
+        keys = [k for k in st.as_dict().keys() if k != "kernel_ms"]
         vec = torch.tensor([float(st.as_dict()[k]) for k in keys], dtype=torch.float64, device="cuda")
-        kms = torch.tensor([st.kernel_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(vec)
         stats = {k: float(v) for k, v in zip(keys, vec.tolist())}
         stats["kernel_ms"] = float(st.kernel_ms)

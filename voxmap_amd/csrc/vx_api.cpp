@@ -7,6 +7,7 @@
 // and math.js:16-49 in double precision, as the JS computes them.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -43,6 +44,9 @@ struct vx_scene {
     unsigned long long *d_stats = nullptr;
     int *d_tiles = nullptr;
     int tiles_cap = 0;
+    int *d_detile = nullptr;
+    int detile_cap = 0;
+    std::vector<int> h_tiles, h_detile;   // last lists uploaded to d_tiles / d_detile
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -158,6 +162,7 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
+    if (s->d_detile) (void)hipFree(s->d_detile);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -267,6 +272,27 @@ int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void
     return rc;
 }
 
+}  // extern "C"
+
+// Tile-id lists live on the device; a list is re-uploaded only when it
+// changes (steady-state frames re-use it), after draining the stream so an
+// in-flight kernel never sees the buffer change under it.
+static int upload_ids(hipStream_t st, const int *ids, int n, int **d_buf, int *cap, std::vector<int> &last) {
+    if ((int)last.size() == n && std::equal(last.begin(), last.end(), ids)) return VX_OK;
+    VX_HIP(hipStreamSynchronize(st));
+    if (n > *cap) {
+        if (*d_buf) VX_HIP(hipFree(*d_buf));
+        *d_buf = nullptr;
+        VX_HIP(hipMalloc(d_buf, sizeof(int) * n));
+        *cap = n;
+    }
+    VX_HIP(hipMemcpy(*d_buf, ids, sizeof(int) * n, hipMemcpyHostToDevice));
+    last.assign(ids, ids + n);
+    return VX_OK;
+}
+
+extern "C" {
+
 int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts, const int *tile_ids, int n_tiles,
                     int fmt, void *out_device, void *stream, vx_stats *stats) {
     int rc = check_params(s, p, w, h, fmt);
@@ -278,13 +304,8 @@ int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts,
         if (tile_ids[i] < 0 || tile_ids[i] >= tx * ty) return set_error(VX_EINVAL, "tile id out of range");
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    if (n_tiles > s->tiles_cap) {
-        if (s->d_tiles) VX_HIP(hipFree(s->d_tiles));
-        s->d_tiles = nullptr;
-        VX_HIP(hipMalloc(&s->d_tiles, sizeof(int) * n_tiles));
-        s->tiles_cap = n_tiles;
-    }
-    VX_HIP(hipMemcpyAsync(s->d_tiles, tile_ids, sizeof(int) * n_tiles, hipMemcpyHostToDevice, st));
+    rc = upload_ids(st, tile_ids, n_tiles, &s->d_tiles, &s->tiles_cap, s->h_tiles);
+    if (rc) return rc;
     return do_render(s, p, w, h, ts, s->d_tiles, n_tiles, fmt, out_device, st, stats);
 }
 
@@ -294,12 +315,9 @@ int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tile
         return set_error(VX_EINVAL, "vx_detile: bad arguments");
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    int *d_ids = nullptr;
-    VX_HIP(hipMallocAsync(&d_ids, sizeof(int) * n_tiles, st));
-    VX_HIP(hipMemcpyAsync(d_ids, tile_ids, sizeof(int) * n_tiles, hipMemcpyHostToDevice, st));
-    int rc = launch_detile(tiles_device, frame_device, w, h, ts, (w + ts - 1) / ts, d_ids, n_tiles, fmt, st);
-    (void)hipFreeAsync(d_ids, st);
-    VX_HIP(hipStreamSynchronize(st));
+    int rc = upload_ids(st, tile_ids, n_tiles, &s->d_detile, &s->detile_cap, s->h_detile);
+    if (rc) return rc;
+    rc = launch_detile(tiles_device, frame_device, w, h, ts, (w + ts - 1) / ts, s->d_detile, n_tiles, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("detile failed: ") + hipGetErrorString((hipError_t)rc));
     return VX_OK;
 }
