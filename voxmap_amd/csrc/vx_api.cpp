@@ -134,7 +134,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
         (e = hipMalloc(&s->d_field, field_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
-        (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT)) != hipSuccess ||
+        (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
         (e = hipMemcpyAsync(s->d_field, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(s->d_noise, noise.data(), noise_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) {
@@ -231,9 +231,10 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.out = out_dev;
     a.p = *p;
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
+    frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
     if (stats) {
         a.stats = s->d_stats;
-        VX_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(unsigned long long) * ST_COUNT, st));
+        VX_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(unsigned long long) * ST_COUNT * 64, st));
     }
     VX_HIP(hipEventRecord(s->ev0, st));
     int rc = launch_render(a, fmt, st);

@@ -11,6 +11,30 @@ namespace vx {
 // message in a thread-local buffer (vx_last_error).
 int set_error(int code, const std::string &msg);
 
+// Per-frame constants derived on the host from vx_frame_params with the same
+// fp32 operations (same order, IEEE, no contraction) the oracle performs per
+// pixel, so the kernel reads bit-identical values.
+struct FrameConsts {
+    int cam_cell[3];
+    float cam_fract[3];
+    float fwd[3], right[3], up[3];
+    float fw, fh, rcp_w, rcp_h;        // (float)w, (float)h and RN(1/w), RN(1/h)
+    float sun[3];                      // u_sunDir
+    float sun_sign[3];                 // sign(u_sunDir) (render.frag:94)
+    float sun_abs[3], sun_rcp[3];      // |u_sunDir|, RN(1/|u_sunDir|)
+    int sun_up;                        // u_sunDir.z > 0: march reads R, else G (render.frag:89)
+    int march_fast;                    // every 2^-10 <= |u_sunDir_i|: fast exact march path
+    int max_steps;                     // MAX_STEPS = 2*Z (render.frag:12)
+    float scatterCol[3], spaceCol[3], shadeCol[3];   // render.frag:168-170, 220
+    float shadeFactor[6];              // per normal index (render.frag:228-229)
+    float normalCol[6][3];             // per normal index (render.frag:211-217)
+    float sf[3];                       // Sf = 1/dims (render.h:24)
+    float cloudTime;                   // u_time * 4e-3 (render.frag:183)
+    float skyOff[2];                   // 1e-4 * (u_cellPos.xy + u_fractPos.xy) (render.frag:191)
+    int quality;
+    unsigned flags;
+};
+
 // Parameters of one render launch (passed by value to the kernel).
 struct KernelArgs {
     const uint32_t *field;   // RGBA8 texels, x fastest (render.js:62)
@@ -26,7 +50,10 @@ struct KernelArgs {
     unsigned long long *stats;   // device counters (nullptr = no stats)
     vx_frame_params p;
     int max_shadow_steps;
+    FrameConsts fc;
 };
+
+void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, int max_steps, FrameConsts &fc);
 
 enum StatSlot {
     ST_PIXELS = 0, ST_SKY, ST_BLOCK, ST_GLASS, ST_PRIM_FETCH, ST_SHADOW_RAYS, ST_SHADOW_FETCH,

@@ -7,37 +7,55 @@
 // 16x16 tile, so the rays of a wave march through neighbouring cells.
 //
 // Numerical contract: fp32, IEEE div/sqrt, no FMA contraction
-// (built with -ffp-contract=off), GLSL built-ins spelled out, vx_exp2 below,
-// so every pixel matches the scalar oracle (oracle/vxo_render.c) bit for bit.
+// (built with -ffp-contract=off), GLSL built-ins spelled out, vexp2 below, so
+// every pixel matches the scalar oracle (oracle/vxo_render.c) bit for bit.
+// Exactness-preserving rewrites used here (each justified in DESIGN.md §5):
+//   * a / b with b a per-frame constant -> two Markstein corrections from
+//     y = RN(1/b) computed on the host (exhaustively checked:
+//     tools/markstein_check.c);
+//   * length(m*t) with a single selected axis -> t (sqrt(RN(t*t)) == t);
+//   * unorm8 decode b/255 -> a 256-entry LDS table of the IEEE quotients;
+//   * per-frame uniform-only expressions -> host (vx_frame.cpp).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
 #include "vx_internal.h"
 
 namespace vx {
 namespace {
 
 constexpr int kGlass = 21;  // render.vert:21, sdf.cpp:337
+constexpr float kInf = __builtin_inff();
 
 // ---------------- GLSL built-ins (GLSL ES 3.00 §8) ----------------
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
 __device__ __forceinline__ float gclamp(float x, float a, float b) { return gmin(gmax(x, a), b); }
 __device__ __forceinline__ float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
-__device__ __forceinline__ float gsign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+// ivec(float) of the contract: NaN -> 0, saturate at +-2^24 (branch-free)
 __device__ __forceinline__ int f2i(float x) {
-    if (x != x) return 0;
-    if (x > 16777216.0f) return 16777216;
-    if (x < -16777216.0f) return -16777216;
-    return (int)x;
+    const float c = __builtin_fminf(__builtin_fmaxf(x, -16777216.0f), 16777216.0f);
+    const int r = (int)c;
+    return x == x ? r : 0;
+}
+
+// a / b, b a per-frame constant with y = RN(1/b): exactly the IEEE quotient
+// (q1 is faithful, Markstein's theorem makes q2 correctly rounded).
+__device__ __forceinline__ float div_const(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r0 = __builtin_fmaf(-q0, b, a);
+    const float q1 = __builtin_fmaf(r0, y, q0);
+    const float r1 = __builtin_fmaf(-q1, b, a);
+    return __builtin_fmaf(r1, y, q1);
 }
 
 // exp2 by the fixed degree-9 polynomial of the numerical contract.
 __device__ __forceinline__ float vexp2(float x) {
     if (x != x) return x;
-    if (x >= 128.0f) return __builtin_inff();
+    if (x >= 128.0f) return kInf;
     if (x < -126.0f) return 0.0f;
-    float n = floorf(x);
-    float f = x - n;
+    const float n = floorf(x);
+    const float f = x - n;
     float p = 1.0178086e-07f;
     p = p * f + 1.3215487e-06f;
     p = p * f + 1.5252734e-05f;
@@ -77,12 +95,12 @@ __constant__ float kPalette[22][3] = {
     {0.505882f, 0.780392f, 0.831373f},
 };
 
-struct Surf {            // one G-buffer record (render.vert outputs)
+struct Surf {            // one G-buffer record (what render.vert hands render.frag)
     int id;              // 0 block, 1 sky, 2 glass
-    int color;
-    int nidx;            // normal index 0..5
-    int cell[3];
-    float fr[3];
+    int color;           // palette index
+    int nidx;            // normal index 0..5 (render.vert:14-17)
+    int c0, c1, c2;      // v_cellPos
+    float f0, f1, f2;    // v_fractPos
 };
 
 struct Counters {
@@ -90,139 +108,195 @@ struct Counters {
 };
 
 __device__ __forceinline__ uint32_t texel(const KernelArgs &a, int x, int y, int z) {
-    return a.field[(size_t)x + (size_t)a.X * ((size_t)y + (size_t)a.Y * (size_t)z)];
+    return a.field[(unsigned)x + (unsigned)a.X * ((unsigned)y + (unsigned)a.Y * (unsigned)z)];
 }
-__device__ __forceinline__ float unorm(uint32_t b) { return (float)b / 255.0f; }
 
 // ---------------- sun march: render.frag:75-142 ----------------
-// Returns true when the ray reaches MAX_STEPS (lit, render.frag:234).
-__device__ bool march_lit(const KernelArgs &a, const int cell[3], const float fr[3], const float r[3],
-                          int max_steps, unsigned &fetches) {
-    int c0 = cell[0], c1 = cell[1], c2 = cell[2];
-    float f0 = fr[0], f1 = fr[1], f2 = fr[2];
-    const float s0 = gsign(r[0]), s1 = gsign(r[1]), s2 = gsign(r[2]);
-    const float a0 = fabsf(r[0]), a1 = fabsf(r[1]), a2 = fabsf(r[2]);
-    const int ch = r[2] > 0.0f ? 0 : 8;   // sdf_dir: R (up) for up-going rays, else G
+// Fast exact path for sun directions with every |r_i| >= 2^-10 (no zero
+// component, so no 0*inf NaN; every t finite and < 1025).  CH = channel read
+// by sdf_dir (0: R "up" for r.z > 0, 1: G "down").  Returns "lit"
+// (step == MAX_STEPS, render.frag:234).
+template <int CH>
+__device__ bool march_fast(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2,
+                           unsigned &fetches) {
+    const FrameConsts &F = a.fc;
+    const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
+    const float b0 = F.sun_abs[0], b1 = F.sun_abs[1], b2 = F.sun_abs[2];
+    const float y0 = F.sun_rcp[0], y1 = F.sun_rcp[1], y2 = F.sun_rcp[2];
+    const float r0 = F.sun[0], r1 = F.sun[1], r2 = F.sun[2];
+    const int maxs = F.max_steps;
     float safe = 1.0f;
     int step = 0;
-    while (step < max_steps && safe != 0.0f) {
-        float x0 = -f0 * s0, x1 = -f1 * s1, x2 = -f2 * s2;
-        float d0 = (x0 - floorf(x0)) + 1e-4f;
-        float d1 = (x1 - floorf(x1)) + 1e-4f;
-        float d2 = (x2 - floorf(x2)) + 1e-4f;
-        float t0 = d0 / a0, t1 = d1 / a1, t2 = d2 / a2;
-        float m0 = t0 <= gmin(t1, t2) ? 1.0f : 0.0f;
-        float m1 = t1 <= gmin(t2, t0) ? 1.0f : 0.0f;
-        float m2 = t2 <= gmin(t0, t1) ? 1.0f : 0.0f;
-        float v0 = m0 * t0, v1 = m1 * t1, v2 = m2 * t2;
-        float len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
-        f0 += r[0] * safe * len;
-        f1 += r[1] * safe * len;
-        f2 += r[2] * safe * len;
-        float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
+    while (step < maxs && safe != 0.0f) {
+        const float x0 = -f0 * s0, x1 = -f1 * s1, x2 = -f2 * s2;                  // :94
+        const float d0 = (x0 - floorf(x0)) + 1e-4f;
+        const float d1 = (x1 - floorf(x1)) + 1e-4f;
+        const float d2 = (x2 - floorf(x2)) + 1e-4f;
+        const float t0 = div_const(d0, b0, y0);                                  // :97
+        const float t1 = div_const(d1, b1, y1);
+        const float t2 = div_const(d2, b2, y2);
+        const float m12 = __builtin_fminf(t1, t2), m20 = __builtin_fminf(t2, t0), m01 = __builtin_fminf(t0, t1);
+        const bool m0 = t0 <= m12, m1 = t1 <= m20, m2 = t2 <= m01;              // :100-104
+        float len = __builtin_fminf(t0, m12);                                    // :105, one axis
+        if ((int)m0 + (int)m1 + (int)m2 > 1) {                                   // ties: literal length
+            const float v0 = m0 ? t0 : 0.0f, v1 = m1 ? t1 : 0.0f, v2 = m2 ? t2 : 0.0f;
+            len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+        }
+        f0 = f0 + (r0 * safe) * len;                                             // :118
+        f1 = f1 + (r1 * safe) * len;
+        f2 = f2 + (r2 * safe) * len;
+        const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
+        c0 += (int)fl0; c1 += (int)fl1; c2 += (int)fl2;                          // :119
+        f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;                             // :120
+        if ((unsigned)c0 >= (unsigned)a.X || (unsigned)c1 >= (unsigned)a.Y || (unsigned)c2 >= (unsigned)a.Z)
+            return true;                                                          // :123-126 sky
+        const uint32_t t = texel(a, c0, c1, c2);                                  // :128
+        fetches++;
+        safe = CH == 0 ? (float)(t & 0xffu) : (float)((t >> 8) & 0xffu);
+        step++;
+    }
+    return step == maxs;
+}
+
+// Literal path for any other sun direction (zero or tiny components: the
+// 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
+__device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2,
+                              unsigned &fetches) {
+    const FrameConsts &F = a.fc;
+    const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
+    const float a0 = F.sun_abs[0], a1 = F.sun_abs[1], a2 = F.sun_abs[2];
+    const float r0 = F.sun[0], r1 = F.sun[1], r2 = F.sun[2];
+    const int sh = F.sun_up ? 0 : 8;
+    const int maxs = F.max_steps;
+    float safe = 1.0f;
+    int step = 0;
+    while (step < maxs && safe != 0.0f) {
+        const float x0 = -f0 * s0, x1 = -f1 * s1, x2 = -f2 * s2;
+        const float d0 = (x0 - floorf(x0)) + 1e-4f;
+        const float d1 = (x1 - floorf(x1)) + 1e-4f;
+        const float d2 = (x2 - floorf(x2)) + 1e-4f;
+        const float t0 = d0 / a0, t1 = d1 / a1, t2 = d2 / a2;
+        const float m0 = t0 <= gmin(t1, t2) ? 1.0f : 0.0f;
+        const float m1 = t1 <= gmin(t2, t0) ? 1.0f : 0.0f;
+        const float m2 = t2 <= gmin(t0, t1) ? 1.0f : 0.0f;
+        const float v0 = m0 * t0, v1 = m1 * t1, v2 = m2 * t2;
+        const float len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+        f0 = f0 + (r0 * safe) * len;
+        f1 = f1 + (r1 * safe) * len;
+        f2 = f2 + (r2 * safe) * len;
+        const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
         c0 += f2i(fl0); c1 += f2i(fl1); c2 += f2i(fl2);
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;
         if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) return true;
-        uint32_t t = texel(a, c0, c1, c2);
+        const uint32_t t = texel(a, c0, c1, c2);
         fetches++;
-        safe = (float)((t >> ch) & 0xffu);   // unorm8 * 255 == b exactly; mix() selects a channel
+        safe = (float)((t >> sh) & 0xffu);
         step++;
     }
-    return step == max_steps;
+    return step == maxs;
 }
 
 // ---------------- primary visibility ----------------
-// First in-grid colour change along the view ray (faces of the greedy mesh of
-// sdf.cpp:281-356 after back-face culling); Chebyshev skips in air cells.
-// Returns number of records (0 sky, 1 surface, 2 glass + what is behind).
-__device__ int primary(const KernelArgs &a, const float d[3], Surf g[2], Counters &cnt) {
-    const int dims[3] = {a.X, a.Y, a.Z};
-    const float *o = a.p.cam_fract;
-    const int *cc = a.p.cam_cell;
-    float inv[3];
-    int stp[3];
-    float tlo = 0.0f, thi = __builtin_inff();
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        stp[i] = d[i] > 0.0f ? 1 : -1;
-        float lo = (float)(0 - cc[i]) - o[i];
-        float hi = (float)(dims[i] - cc[i]) - o[i];
-        if (d[i] != 0.0f) {
-            inv[i] = 1.0f / d[i];
-            float t0 = lo * inv[i], t1 = hi * inv[i];
-            if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
-            tlo = gmax(tlo, t0);
-            thi = gmin(thi, t1);
-        } else {
-            inv[i] = 0.0f;
-            if (!(lo <= 0.0f && 0.0f < hi)) return 0;
-        }
+// First in-grid colour change along the view ray = the nearest front face of
+// the greedy mesh of sdf.cpp:281-356 after back-face culling; in air cells
+// with Chebyshev distance D >= 3 (A byte) the ray jumps (D-1.5)/|d|_inf.
+// Camera-relative cells; returns 0 sky, 1 surface, 2 glass + what is behind.
+__device__ __forceinline__ float tmax_of(int c, int st, float o, float d, float iv) {
+    return d != 0.0f ? ((float)(c + (st > 0 ? 1 : 0)) - o) * iv : kInf;
+}
+
+__device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &g0, Surf &g1, Counters &cnt) {
+    const FrameConsts &F = a.fc;
+    const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
+    const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
+    const int st0 = d0 > 0.0f ? 1 : -1, st1 = d1 > 0.0f ? 1 : -1, st2 = d2 > 0.0f ? 1 : -1;
+    float tlo = 0.0f, thi = kInf;
+    float iv0 = 0.0f, iv1 = 0.0f, iv2 = 0.0f;
+    bool miss = false;
+    {
+        const float lo = (float)(0 - cc0) - o0, hi = (float)(a.X - cc0) - o0;
+        if (d0 != 0.0f) {
+            iv0 = 1.0f / d0;
+            float t0 = lo * iv0, t1 = hi * iv0;
+            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
+            tlo = gmax(tlo, t0); thi = gmin(thi, t1);
+        } else miss |= !(lo <= 0.0f && 0.0f < hi);
     }
-    if (!(tlo < thi)) return 0;
-    const float amax = gmax(gmax(fabsf(d[0]), fabsf(d[1])), fabsf(d[2]));
-    const float inv_inf = 1.0f / amax;
-    int c[3];
-    float tmax[3];
+    {
+        const float lo = (float)(0 - cc1) - o1, hi = (float)(a.Y - cc1) - o1;
+        if (d1 != 0.0f) {
+            iv1 = 1.0f / d1;
+            float t0 = lo * iv1, t1 = hi * iv1;
+            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
+            tlo = gmax(tlo, t0); thi = gmin(thi, t1);
+        } else miss |= !(lo <= 0.0f && 0.0f < hi);
+    }
+    {
+        const float lo = (float)(0 - cc2) - o2, hi = (float)(a.Z - cc2) - o2;
+        if (d2 != 0.0f) {
+            iv2 = 1.0f / d2;
+            float t0 = lo * iv2, t1 = hi * iv2;
+            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
+            tlo = gmax(tlo, t0); thi = gmin(thi, t1);
+        } else miss |= !(lo <= 0.0f && 0.0f < hi);
+    }
+    if (miss || !(tlo < thi)) return 0;
+    const float inv_inf = 1.0f / gmax(gmax(fabsf(d0), fabsf(d1)), fabsf(d2));
     float tcur = tlo;
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        float p = o[i] + tcur * d[i];
-        int ci = f2i(floorf(p));
-        int lo = -cc[i], hi = dims[i] - cc[i] - 1;
-        c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-        tmax[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? 1 : 0)) - o[i]) * inv[i] : __builtin_inff();
-    int nrec = 0;
-    uint32_t t = texel(a, c[0] + cc[0], c[1] + cc[1], c[2] + cc[2]);
+    int c0 = min(max((int)floorf(o0 + tcur * d0), -cc0), a.X - cc0 - 1);
+    int c1 = min(max((int)floorf(o1 + tcur * d1), -cc1), a.Y - cc1 - 1);
+    int c2 = min(max((int)floorf(o2 + tcur * d2), -cc2), a.Z - cc2 - 1);
+    float tm0 = tmax_of(c0, st0, o0, d0, iv0), tm1 = tmax_of(c1, st1, o1, d1, iv1), tm2 = tmax_of(c2, st2, o2, d2, iv2);
+    uint32_t t = texel(a, c0 + cc0, c1 + cc1, c2 + cc2);
     cnt.prim_fetch++;
     int prev = (t >> 16) & 0xff;
     int dist = t >> 24;
-    const int cap = 4 * (dims[0] + dims[1] + dims[2]);
+    int nrec = 0;
+    const int cap = 4 * (a.X + a.Y + a.Z);
     for (int iter = 0; iter < cap; iter++) {
-        if (prev == 0 && dist >= 3) {
+        const bool skip = prev == 0 && dist >= 3;
+        bool s0 = false, s1 = false, s2 = false;
+        float tcross = 0.0f;
+        if (skip) {
             tcur = tcur + ((float)dist - 1.5f) * inv_inf;
-#pragma unroll
-            for (int i = 0; i < 3; i++) {
-                float p = o[i] + tcur * d[i];
-                c[i] = f2i(floorf(p));
-                tmax[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? 1 : 0)) - o[i]) * inv[i] : __builtin_inff();
-            }
-            int x = c[0] + cc[0], y = c[1] + cc[1], z = c[2] + cc[2];
-            if (x < 0 || y < 0 || z < 0 || x >= a.X || y >= a.Y || z >= a.Z) return nrec;
-            t = texel(a, x, y, z);
-            cnt.prim_fetch++;
-            dist = t >> 24;
-            continue;
+            c0 = (int)floorf(o0 + tcur * d0);
+            c1 = (int)floorf(o1 + tcur * d1);
+            c2 = (int)floorf(o2 + tcur * d2);
+            tm0 = tmax_of(c0, st0, o0, d0, iv0);
+            tm1 = tmax_of(c1, st1, o1, d1, iv1);
+            tm2 = tmax_of(c2, st2, o2, d2, iv2);
+        } else {
+            s0 = tm0 <= tm1 && tm0 <= tm2;
+            s1 = !s0 && tm1 <= tm2;
+            s2 = !s0 && !s1;
+            tcross = s0 ? tm0 : (s1 ? tm1 : tm2);
+            if (s0) { c0 += st0; tm0 = ((float)(c0 + (st0 > 0 ? 1 : 0)) - o0) * iv0; }
+            if (s1) { c1 += st1; tm1 = ((float)(c1 + (st1 > 0 ? 1 : 0)) - o1) * iv1; }
+            if (s2) { c2 += st2; tm2 = ((float)(c2 + (st2 > 0 ? 1 : 0)) - o2) * iv2; }
+            tcur = tcross;
         }
-        int ax = (tmax[0] <= tmax[1] && tmax[0] <= tmax[2]) ? 0 : (tmax[1] <= tmax[2] ? 1 : 2);
-        float tcross = tmax[ax];
-        c[ax] += stp[ax];
-        tmax[ax] = ((float)(c[ax] + (stp[ax] > 0 ? 1 : 0)) - o[ax]) * inv[ax];
-        tcur = tcross;
-        int ac[3] = {c[0] + cc[0], c[1] + cc[1], c[2] + cc[2]};
-        if (ac[0] < 0 || ac[1] < 0 || ac[2] < 0 || ac[0] >= a.X || ac[1] >= a.Y || ac[2] >= a.Z) return nrec;
-        t = texel(a, ac[0], ac[1], ac[2]);
+        const int x = c0 + cc0, y = c1 + cc1, z = c2 + cc2;
+        if ((unsigned)x >= (unsigned)a.X || (unsigned)y >= (unsigned)a.Y || (unsigned)z >= (unsigned)a.Z)
+            return nrec;                                           // left the grid: sky behind
+        t = texel(a, x, y, z);
         cnt.prim_fetch++;
-        int col = (t >> 16) & 0xff;
         dist = t >> 24;
+        if (skip) continue;                                        // the skip cannot leave air
+        const int col = (t >> 16) & 0xff;
         if (col != prev) {
-            Surf &h = g[nrec];
+            Surf h;
             h.color = col;
             h.id = col == kGlass ? 2 : 0;
-            h.nidx = 2 * ax + (stp[ax] > 0 ? 1 : 0);
-#pragma unroll
-            for (int i = 0; i < 3; i++) {
-                if (i == ax) {
-                    h.cell[i] = ac[i] + (stp[ax] > 0 ? 0 : 1);
-                    h.fr[i] = 0.0f;
-                } else {
-                    float p = o[i] + tcross * d[i];
-                    h.cell[i] = ac[i];
-                    h.fr[i] = p - (float)c[i];
-                }
-            }
+            const int st = s0 ? st0 : (s1 ? st1 : st2);
+            h.nidx = (s0 ? 0 : (s1 ? 2 : 4)) + (st > 0 ? 1 : 0);
+            const int up = st > 0 ? 0 : 1;
+            h.c0 = x + (s0 ? up : 0);
+            h.c1 = y + (s1 ? up : 0);
+            h.c2 = z + (s2 ? up : 0);
+            h.f0 = s0 ? 0.0f : (o0 + tcross * d0) - (float)c0;
+            h.f1 = s1 ? 0.0f : (o1 + tcross * d1) - (float)c1;
+            h.f2 = s2 ? 0.0f : (o2 + tcross * d2) - (float)c2;
+            if (nrec == 0) g0 = h; else g1 = h;
             nrec++;
             if (h.id != 2 || nrec == 2) return nrec;
         }
@@ -234,205 +308,174 @@ __device__ int primary(const KernelArgs &a, const float d[3], Surf g[2], Counter
 
 // ---------------- sampling ----------------
 __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1, float &w) {
-    float u = coord * (float)size - 0.5f;
-    float fl = floorf(u);
+    const float u = coord * (float)size - 0.5f;
+    const float fl = floorf(u);
     w = u - fl;
-    int i = f2i(fl);
-    int j = i + 1;
-    i0 = i < 0 ? 0 : (i > size - 1 ? size - 1 : i);
-    i1 = j < 0 ? 0 : (j > size - 1 ? size - 1 : j);
+    const int i = f2i(fl);
+    const int j = i + 1;
+    i0 = min(max(i, 0), size - 1);
+    i1 = min(max(j, 0), size - 1);
 }
 
-// sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G (LOD 0).
-__device__ float sdf_lin(const KernelArgs &a, const int c[3], const float f[3]) {
-    const int dims[3] = {a.X, a.Y, a.Z};
-    int i0[3], i1[3];
-    float w[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        float sf = 1.0f / (float)dims[k];
-        float coord = ((float)c[k] + f[k]) * sf;
-        lin_axis(coord, dims[k], i0[k], i1[k], w[k]);
-    }
-    uint32_t t[2][2][2];
-#pragma unroll
-    for (int kz = 0; kz < 2; kz++)
-#pragma unroll
-        for (int ky = 0; ky < 2; ky++)
-#pragma unroll
-            for (int kx = 0; kx < 2; kx++)
-                t[kz][ky][kx] = texel(a, kx ? i1[0] : i0[0], ky ? i1[1] : i0[1], kz ? i1[2] : i0[2]);
+// sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G at LOD 0.
+__device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
+    const FrameConsts &F = a.fc;
+    int x0, x1, y0, y1, z0, z1;
+    float wx, wy, wz;
+    lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
+    lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
+    lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
+    const uint32_t t000 = texel(a, x0, y0, z0), t100 = texel(a, x1, y0, z0);
+    const uint32_t t010 = texel(a, x0, y1, z0), t110 = texel(a, x1, y1, z0);
+    const uint32_t t001 = texel(a, x0, y0, z1), t101 = texel(a, x1, y0, z1);
+    const uint32_t t011 = texel(a, x0, y1, z1), t111 = texel(a, x1, y1, z1);
     float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
-        float v[2][2];
-#pragma unroll
-        for (int kz = 0; kz < 2; kz++)
-#pragma unroll
-            for (int ky = 0; ky < 2; ky++)
-                v[kz][ky] = gmix(unorm((t[kz][ky][0] >> (8 * ch)) & 0xffu),
-                                 unorm((t[kz][ky][1] >> (8 * ch)) & 0xffu), w[0]);
-        float w0 = gmix(v[0][0], v[0][1], w[1]);
-        float w1 = gmix(v[1][0], v[1][1], w[1]);
-        res[ch] = gmix(w0, w1, w[2]) * 255.0f;
+        const int sh = 8 * ch;
+        const float v00 = gmix(unorm[(t000 >> sh) & 0xff], unorm[(t100 >> sh) & 0xff], wx);
+        const float v01 = gmix(unorm[(t010 >> sh) & 0xff], unorm[(t110 >> sh) & 0xff], wx);
+        const float v10 = gmix(unorm[(t001 >> sh) & 0xff], unorm[(t101 >> sh) & 0xff], wx);
+        const float v11 = gmix(unorm[(t011 >> sh) & 0xff], unorm[(t111 >> sh) & 0xff], wx);
+        const float w0 = gmix(v00, v01, wy);
+        const float w1 = gmix(v10, v11, wy);
+        res[ch] = gmix(w0, w1, wz) * 255.0f;
     }
     return gmin(res[0], res[1]);
 }
 
 __device__ __forceinline__ int wrap_idx(float fl, int n) {
-    float q = floorf(fl / (float)n);
+    const float q = floorf(fl / (float)n);
     return f2i(fl - q * (float)n) & (n - 1);
 }
 
-// fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT.
-__device__ float fbm(const KernelArgs &a, float px, float py) {
+// fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT, LOD 0.
+__device__ float fbm(const KernelArgs &a, const float *unorm, float px, float py) {
     const int W = a.noise_w, H = a.noise_h;
-    float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
-    float fu = floorf(u), fv = floorf(v);
-    float wa = u - fu, wb = v - fv;
-    int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
-    int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-    float t00 = unorm(a.noise[(size_t)y0 * W + x0] >> 24);
-    float t10 = unorm(a.noise[(size_t)y0 * W + x1] >> 24);
-    float t01 = unorm(a.noise[(size_t)y1 * W + x0] >> 24);
-    float t11 = unorm(a.noise[(size_t)y1 * W + x1] >> 24);
-    float r0 = gmix(t00, t10, wa), r1 = gmix(t01, t11, wa);
-    float t = gmix(r0, r1, wb);
-    return 1.0f - 2.0f * t;
+    const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
+    const float fu = floorf(u), fv = floorf(v);
+    const float wa = u - fu, wb = v - fv;
+    const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
+    const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+    const float t00 = unorm[a.noise[(unsigned)y0 * W + x0] >> 24];
+    const float t10 = unorm[a.noise[(unsigned)y0 * W + x1] >> 24];
+    const float t01 = unorm[a.noise[(unsigned)y1 * W + x0] >> 24];
+    const float t11 = unorm[a.noise[(unsigned)y1 * W + x1] >> 24];
+    const float r0 = gmix(t00, t10, wa), r1 = gmix(t01, t11, wa);
+    return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
 
-__device__ __forceinline__ float dot3(const float x[3], const float y[3]) {
-    return x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
-}
-__device__ __forceinline__ void normalize3(const float v[3], float out[3]) {
-    float l = sqrtf(dot3(v, v));
-    out[0] = v[0] / l; out[1] = v[1] / l; out[2] = v[2] / l;
+__device__ __forceinline__ void normalize3(float v0, float v1, float v2, float &o0, float &o1, float &o2) {
+    const float l = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    o0 = v0 / l; o1 = v1 / l; o2 = v2 / l;
 }
 
-// ---------------- render.frag main() (render.frag:147-252) ----------------
-__device__ void shade(const KernelArgs &a, const Surf &g, const float prim_dir[3], float o[4],
-                      Counters &cnt) {
-    const vx_frame_params &P = a.p;
-    o[0] = 0.0f; o[1] = 0.0f; o[2] = 0.0f; o[3] = 1.0f;
-    const bool isSky = g.id == 1, isGlass = g.id == 2;
-    const float litCol[3] = {0.4f, 0.35f, 0.3f};
-    float nrm[3] = {0.0f, 0.0f, 0.0f};
-    const int ni = isSky ? 1 : g.nidx;
-    nrm[ni >> 1] = (ni & 1) ? -1.0f : 1.0f;
-    float rayDir[3];
-    if (isSky) {
-        normalize3(prim_dir, rayDir);
-    } else {
-        float v[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++) v[i] = (float)(g.cell[i] - P.cam_cell[i]) + (g.fr[i] - P.cam_fract[i]);
-        normalize3(v, rayDir);
-    }
-    float refl[3];
-    {
-        float k = 2.0f * dot3(nrm, rayDir);
-#pragma unroll
-        for (int i = 0; i < 3; i++) refl[i] = rayDir[i] - k * nrm[i];
-    }
+// ---------------- render.frag main(), sky branch (render.frag:148-205) ----------------
+__device__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, float d1, float d2, float o[4],
+                          Counters &cnt) {
+    const FrameConsts &F = a.fc;
+    float r0, r1, r2;
+    normalize3(d0, d1, d2, r0, r1, r2);          // skybox modelled at infinity
+    // reflect(rayDir, (-1,0,0)) (render.frag:155); only .z is read
+    const float k = 2.0f * ((-1.0f * r0 + 0.0f * r1) + 0.0f * r2);
+    const float refl_z = r2 - k * 0.0f;
     const float sunCol[3] = {1.4f, 1.0f, 0.5f};
-    float sunFactor = gmax(0.0f, dot3(P.sun_dir, rayDir)) - 1.0f;
-    float glow = vexp2(8.0f * sunFactor);
+    float sunFactor = gmax(0.0f, F.sun[0] * r0 + F.sun[1] * r1 + F.sun[2] * r2) - 1.0f;
+    const float glow = vexp2(8.0f * sunFactor);
     sunFactor = vexp2(4000.0f * sunFactor) + 0.3f * glow;
-    float scatter = 1.0f - sqrtf(gmax(0.0f, P.sun_dir[2]));
-    const float sp0[3] = {0.2f, 0.4f, 0.7f}, sp1[3] = {0.2f, 0.3f, 0.5f};
-    const float sc0[3] = {0.7f, 0.9f, 1.0f}, sc1[3] = {1.0f, 0.3f, 0.2f};
-    float scatterCol[3], atmCol[3], skyCol[3];
-    float rz = sqrtf(gmax(0.0f, refl[2]));
+    const float rz = sqrtf(gmax(0.0f, refl_z));
+    float sky[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        float spaceCol = gmix(sp0[i], sp1[i], scatter);
-        scatterCol[i] = gmix(sc0[i], sc1[i], scatter);
-        atmCol[i] = gmix(scatterCol[i], spaceCol, rz);
-        skyCol[i] = gclamp(sunCol[i] * sunFactor + atmCol[i], 0.0f, 1.0f);
+        const float atm = gmix(F.scatterCol[i], F.spaceCol[i], rz);
+        sky[i] = gclamp(sunCol[i] * sunFactor + atm, 0.0f, 1.0f);
     }
-    if (isSky) {
-        rayDir[2] = fabsf(rayDir[2]);
-        if (P.flags & VX_FLAG_NO_CLOUDS) {
-            o[0] = skyCol[0]; o[1] = skyCol[1]; o[2] = skyCol[2];
-            return;
-        }
-        cnt.noise_px++;
-        float cloudTime = P.time * 4e-3f;
-        float den = sqrtf(fabsf(rayDir[2]) + 0.03f);
-        float sx = rayDir[0] / den, sy = rayDir[1] / den;
-        sx = sx * 0.1f; sy = sy * 0.1f;
-        float sl = sqrtf(sqrtf(sx * sx + sy * sy));
-        sx = sx * sl; sy = sy * sl;
-        float n0 = fbm(a, 2.0f * sx + cloudTime, 2.0f * sy + cloudTime);
-        float n1 = fbm(a, 2.0f * sx - cloudTime, 2.0f * sy - cloudTime);
-        sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
-        sx = sx + 1e-4f * ((float)P.cam_cell[0] + P.cam_fract[0]);
-        sy = sy + 1e-4f * ((float)P.cam_cell[1] + P.cam_fract[1]);
-        float cloudFactor = vexp2(6.0f * (fbm(a, sx + 2.0f * cloudTime, sy + -9.0f * cloudTime) - 1.0f));
-        float scf = sqrtf(cloudFactor);
-        float mountainPos = rayDir[0] / rayDir[1];
-        float mountainHeight = 1.0f - fbm(a, 0.3f * mountainPos, 0.3f * mountainPos);
-        float mountainFactor = 2.0f - fbm(a, 2.0f * (mountainPos + rayDir[1]), 2.0f * (mountainPos + rayDir[2]));
-        mountainHeight = mountainHeight / (vexp(0.3f * mountainPos * mountainPos) * 6.0f);
-        if (mountainHeight > rayDir[2] && rayDir[1] > 0.0f && rayDir[2] > 0.0f) {
-            const float mt[3] = {0.7f, 0.8f, 0.7f};
-            float w = mountainFactor * rayDir[2];
-#pragma unroll
-            for (int i = 0; i < 3; i++) skyCol[i] = gmix(skyCol[i], skyCol[i] * mt[i], w);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 3; i++) skyCol[i] = gmix(skyCol[i], gmix(sunCol[i], 0.8f, scf), cloudFactor);
-        }
-        o[0] = skyCol[0]; o[1] = skyCol[1]; o[2] = skyCol[2];
+    r2 = fabsf(r2);                                                               // :179
+    if (F.flags & VX_FLAG_NO_CLOUDS) {
+        o[0] = sky[0]; o[1] = sky[1]; o[2] = sky[2]; o[3] = 1.0f;
         return;
     }
-    // block branch (render.frag:207-251)
-    const int pidx = g.color;
-    float base[3];
-    if (pidx < 22) { base[0] = kPalette[pidx][0]; base[1] = kPalette[pidx][1]; base[2] = kPalette[pidx][2]; }
-    else { base[0] = base[1] = base[2] = 1.0f; }
-    const float an0 = fabsf(nrm[0]), an1 = fabsf(nrm[1]), an2 = fabsf(nrm[2]);
-    const float M0[3] = {0.90f, 0.90f, 0.95f}, M1[3] = {0.95f, 0.95f, 1.00f};
-    float normalCol[3];
+    cnt.noise_px++;
+    const float ct = F.cloudTime;
+    const float den = sqrtf(fabsf(r2) + 0.03f);
+    float sx = r0 / den, sy = r1 / den;                                           // :184
+    sx = sx * 0.1f; sy = sy * 0.1f;
+    const float sl = sqrtf(sqrtf(sx * sx + sy * sy));
+    sx = sx * sl; sy = sy * sl;
+    const float n0 = fbm(a, unorm, 2.0f * sx + ct, 2.0f * sy + ct);
+    const float n1 = fbm(a, unorm, 2.0f * sx - ct, 2.0f * sy - ct);
+    sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
+    sx = sx + F.skyOff[0];
+    sy = sy + F.skyOff[1];
+    const float cloudFactor = vexp2(6.0f * (fbm(a, unorm, sx + 2.0f * ct, sy + -9.0f * ct) - 1.0f));
+    const float scf = sqrtf(cloudFactor);
+    const float mountainPos = r0 / r1;                                            // :195
+    float mountainHeight = 1.0f - fbm(a, unorm, 0.3f * mountainPos, 0.3f * mountainPos);
+    const float mountainFactor = 2.0f - fbm(a, unorm, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2));
+    mountainHeight = mountainHeight / (vexp(0.3f * mountainPos * mountainPos) * 6.0f);
+    if (mountainHeight > r2 && r1 > 0.0f && r2 > 0.0f) {
+        const float mt[3] = {0.7f, 0.8f, 0.7f};
+        const float w = mountainFactor * r2;
 #pragma unroll
-    for (int i = 0; i < 3; i++) normalCol[i] = (M0[i] * an0 + M1[i] * an1) + 1.0f * an2;
-    if (nrm[2] < 0.0f) {
+        for (int i = 0; i < 3; i++) sky[i] = gmix(sky[i], sky[i] * mt[i], w);
+    } else {
 #pragma unroll
-        for (int i = 0; i < 3; i++) normalCol[i] = normalCol[i] * 0.8f;
+        for (int i = 0; i < 3; i++) sky[i] = gmix(sky[i], gmix(sunCol[i], 0.8f, scf), cloudFactor);
     }
-    float shadeCol[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) shadeCol[i] = 0.7f * scatterCol[i];
-    float ambCol[3] = {1.0f, 1.0f, 1.0f};
-    if (!(P.flags & VX_FLAG_NO_AO)) {
+    o[0] = sky[0]; o[1] = sky[1]; o[2] = sky[2]; o[3] = 1.0f;
+}
+
+// ---------------- render.frag main(), block branch (render.frag:148-176, 207-251) ----------------
+__device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt) {
+    const FrameConsts &F = a.fc;
+    const int ni = g.nidx;
+    const float n0 = ni == 0 ? 1.0f : (ni == 1 ? -1.0f : 0.0f);
+    const float n1 = ni == 2 ? 1.0f : (ni == 3 ? -1.0f : 0.0f);
+    const float n2 = ni == 4 ? 1.0f : (ni == 5 ? -1.0f : 0.0f);
+    float r0, r1, r2;
+    normalize3((float)(g.c0 - F.cam_cell[0]) + (g.f0 - F.cam_fract[0]),
+               (float)(g.c1 - F.cam_cell[1]) + (g.f1 - F.cam_fract[1]),
+               (float)(g.c2 - F.cam_cell[2]) + (g.f2 - F.cam_fract[2]), r0, r1, r2);   // :154
+    float base0 = 1.0f, base1 = 1.0f, base2 = 1.0f;
+    if (g.color < 22) { base0 = kPalette[g.color][0]; base1 = kPalette[g.color][1]; base2 = kPalette[g.color][2]; }
+    float amb0 = 1.0f, amb1 = 1.0f, amb2 = 1.0f;
+    if (!(F.flags & VX_FLAG_NO_AO)) {                                                  // :223-225
         cnt.ao++;
-        int ac[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++) ac[i] = g.cell[i] + f2i(nrm[i]);
-        float ambDist = sdf_lin(a, ac, g.fr);
-        float ambFactor = gmin(1.0f - sqrtf(ambDist), 0.8f);
-#pragma unroll
-        for (int i = 0; i < 3; i++) ambCol[i] = gmix(1.0f, shadeCol[i], ambFactor);
+        const float ambDist = sdf_lin(a, unorm, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
+        const float ambFactor = gmin(1.0f - sqrtf(ambDist), 0.8f);
+        amb0 = gmix(1.0f, F.shadeCol[0], ambFactor);
+        amb1 = gmix(1.0f, F.shadeCol[1], ambFactor);
+        amb2 = gmix(1.0f, F.shadeCol[2], ambFactor);
     }
-    float shadeFactor = P.sun_dir[2] < 0.0f ? 0.0f : sqrtf(gmax(0.0f, dot3(nrm, P.sun_dir)));
-    if (shadeFactor > 0.0f && !(P.flags & VX_FLAG_NO_SHADOW)) {
+    float shadeFactor = F.shadeFactor[ni];                                             // :228-229
+    if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
         cnt.shadow_rays++;
-        bool lit = march_lit(a, g.cell, g.fr, P.sun_dir, a.max_shadow_steps, cnt.shadow_fetch);
+        bool lit;
+        if (F.march_fast)
+            lit = F.sun_up ? march_fast<0>(a, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch)
+                           : march_fast<1>(a, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+        else
+            lit = march_literal(a, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
         shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
     }
-    float lightCol[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) lightCol[i] = shadeCol[i] + litCol[i] * shadeFactor;
-#pragma unroll
-    for (int i = 0; i < 3; i++) o[i] = base[i];
-    if (P.quality > 0) {
-#pragma unroll
-        for (int i = 0; i < 3; i++) o[i] = o[i] * ((normalCol[i] * lightCol[i]) * ambCol[i]);
+    const float l0 = F.shadeCol[0] + 0.4f * shadeFactor;                               // :238
+    const float l1 = F.shadeCol[1] + 0.35f * shadeFactor;
+    const float l2 = F.shadeCol[2] + 0.3f * shadeFactor;
+    o[0] = base0; o[1] = base1; o[2] = base2; o[3] = 1.0f;
+    if (F.quality > 0) {                                                               // :242-244
+        o[0] = o[0] * ((F.normalCol[ni][0] * l0) * amb0);
+        o[1] = o[1] * ((F.normalCol[ni][1] * l1) * amb1);
+        o[2] = o[2] * ((F.normalCol[ni][2] * l2) * amb2);
     }
-    if (isGlass) {
-        o[3] = 0.8f * vexp2(dot3(rayDir, nrm));
+    if (g.id == 2) {                                                                   // :246-249
+        const float k = 2.0f * ((n0 * r0 + n1 * r1) + n2 * r2);
+        const float rz = sqrtf(gmax(0.0f, r2 - k * n2));
+        o[3] = 0.8f * vexp2((r0 * n0 + r1 * n1) + r2 * n2);
 #pragma unroll
-        for (int i = 0; i < 3; i++) o[i] = o[i] * (0.2f * atmCol[i]);
+        for (int i = 0; i < 3; i++) {
+            const float atm = gmix(F.scatterCol[i], F.spaceCol[i], rz);
+            o[i] = o[i] * (0.2f * atm);
+        }
     }
 }
 
@@ -445,17 +488,21 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
 
 template <int FMT, bool STATS, bool TILED>
 __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
+    // unorm8 -> float table: b/255 as IEEE quotients (render.frag:38 decode)
+    __shared__ float s_unorm[256];
+    s_unorm[threadIdx.x] = (float)threadIdx.x / 255.0f;
+    __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lx = ((wave & 1) << 3) | (lane & 7);
     const int ly = ((wave >> 1) << 3) | (lane >> 3);
     int px, py;
     size_t out_idx;
     if (TILED) {
-        const int bpt = (a.tile_size >> 4) * (a.tile_size >> 4);  // 16x16 blocks per tile
+        const int sub_per_row = a.tile_size >> 4;
+        const int bpt = sub_per_row * sub_per_row;   // 16x16 blocks per tile
         const int k = blockIdx.x / bpt, sub = blockIdx.x % bpt;
         const int tid = a.tile_ids[k];
-        const int sbx = sub % (a.tile_size >> 4), sby = sub / (a.tile_size >> 4);
-        const int tx = (sbx << 4) + lx, ty = (sby << 4) + ly;
+        const int tx = ((sub % sub_per_row) << 4) + lx, ty = ((sub / sub_per_row) << 4) + ly;
         px = (tid % a.tiles_x) * a.tile_size + tx;
         py = (tid / a.tiles_x) * a.tile_size + ty;
         out_idx = (size_t)k * a.tile_size * a.tile_size + (size_t)ty * a.tile_size + tx;
@@ -464,36 +511,36 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
         py = (blockIdx.y << 4) + ly;
         out_idx = (size_t)py * a.w + px;
     }
+    const FrameConsts &F = a.fc;
     const bool active = px < a.w && py < a.h;
     Counters cnt = {0, 0, 0, 0, 0, 0};
     unsigned n_sky = 0, n_block = 0, n_glass = 0;
-    float rgba[4] = {0.0f, 0.0f, 0.0f, 1.0f};
     if (active) {
-        const float nx = (float)(2 * px + 1) / (float)a.w - 1.0f;
-        const float ny = 1.0f - (float)(2 * py + 1) / (float)a.h;
-        float d[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++) d[i] = (a.p.ray_fwd[i] + nx * a.p.ray_right[i]) + ny * a.p.ray_up[i];
+        // nx = (2px+1)/w - 1, ny = 1 - (2py+1)/h with exact quotients
+        const float nx = div_const((float)(2 * px + 1), F.fw, F.rcp_w) - 1.0f;
+        const float ny = 1.0f - div_const((float)(2 * py + 1), F.fh, F.rcp_h);
+        const float d0 = (F.fwd[0] + nx * F.right[0]) + ny * F.up[0];
+        const float d1 = (F.fwd[1] + nx * F.right[1]) + ny * F.up[1];
+        const float d2 = (F.fwd[2] + nx * F.right[2]) + ny * F.up[2];
         Surf g[2];
-        const int n = primary(a, d, g, cnt);
-        Surf sky;
-        sky.id = 1; sky.color = 0; sky.nidx = 1;
-        sky.cell[0] = sky.cell[1] = sky.cell[2] = 0;
-        sky.fr[0] = sky.fr[1] = sky.fr[2] = 0.0f;
+        const int n = primary(a, d0, d1, d2, g[0], g[1], cnt);
+        float rgba[4];
         if (n == 0) {
             n_sky = 1;
-            shade(a, sky, d, rgba, cnt);
-        } else if (g[0].id != 2) {
-            n_block = 1;
-            shade(a, g[0], d, rgba, cnt);
+            shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
-            n_glass = 1;
-            float src[4], dst[4];
-            shade(a, g[0], d, src, cnt);
-            shade(a, n == 2 ? g[1] : sky, d, dst, cnt);
-            const float al = src[3];
+            shade_block(a, s_unorm, g[0], rgba, cnt);
+            if (g[0].id == 2) {
+                n_glass = 1;
+                float dst[4];
+                if (n == 2) shade_block(a, s_unorm, g[1], dst, cnt);
+                else shade_sky(a, s_unorm, d0, d1, d2, dst, cnt);
+                const float al = rgba[3];
 #pragma unroll
-            for (int i = 0; i < 3; i++) rgba[i] = src[i] * al + dst[i] * (1.0f - al);
+                for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+            } else {
+                n_block = 1;
+            }
         }
         rgba[3] = 1.0f;
         if (FMT == VX_PIXEL_RGBA32F) {
@@ -501,10 +548,7 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
         } else {
             uint32_t pk = 0;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                float v = gclamp(rgba[i], 0.0f, 1.0f) * 255.0f + 0.5f;
-                pk |= (uint32_t)v << (8 * i);
-            }
+            for (int i = 0; i < 4; i++) pk |= (uint32_t)(gclamp(rgba[i], 0.0f, 1.0f) * 255.0f + 0.5f) << (8 * i);
             reinterpret_cast<uint32_t *>(a.out)[out_idx] = pk;
         }
     }
@@ -521,8 +565,10 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
         v[ST_NOISE_PX] = wave_sum(cnt.noise_px);
         v[ST_CAP_HITS] = wave_sum(cnt.cap_hit);
         if (lane == 0) {
+            // spread the adds over 64 slot rows to avoid one hot line per counter
+            unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
 #pragma unroll
-            for (int i = 0; i < ST_COUNT; i++) atomicAdd(a.stats + i, v[i]);
+            for (int i = 0; i < ST_COUNT; i++) atomicAdd(row + i, v[i]);
         }
     }
 }
@@ -560,7 +606,6 @@ __global__ void k_dist_yz(const uint8_t *gin, uint8_t *gout, uint32_t *field, in
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t N = (size_t)X * Y * Z;
     if (i >= N) return;
-    const int x = (int)(i % X);
     const int y = (int)((i / X) % Y);
     const int z = (int)(i / ((size_t)X * Y));
     const int pos = axis == 1 ? y : z, n = axis == 1 ? Y : Z;
@@ -575,12 +620,17 @@ __global__ void k_dist_yz(const uint8_t *gin, uint8_t *gout, uint32_t *field, in
         const int m = v > ak ? v : ak;
         best = m < best ? m : best;
     }
-    if (axis == 1) {
-        gout[i] = (uint8_t)best;
-    } else {
-        field[i] = (field[i] & 0x00ffffffu) | ((uint32_t)best << 24);
+    if (axis == 1) gout[i] = (uint8_t)best;
+    else field[i] = (field[i] & 0x00ffffffu) | ((uint32_t)best << 24);
+}
+
+__global__ void k_reduce_stats(unsigned long long *stats) {
+    const int i = threadIdx.x;
+    if (i < ST_COUNT) {
+        unsigned long long s = 0;
+        for (int r = 0; r < 64; r++) s += stats[r * ST_COUNT + i];
+        stats[i] = s;
     }
-    (void)x;
 }
 
 }  // namespace
@@ -590,11 +640,8 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
     dim3 block(256);
     dim3 grid;
     const bool tiled = a.tile_ids != nullptr;
-    if (tiled) {
-        grid = dim3(a.n_tiles * (a.tile_size >> 4) * (a.tile_size >> 4));
-    } else {
-        grid = dim3((a.w + 15) / 16, (a.h + 15) / 16);
-    }
+    if (tiled) grid = dim3(a.n_tiles * (a.tile_size >> 4) * (a.tile_size >> 4));
+    else grid = dim3((a.w + 15) / 16, (a.h + 15) / 16);
     const bool st = a.stats != nullptr;
 #define VX_LAUNCH(F, S, T) hipLaunchKernelGGL((k_render<F, S, T>), grid, block, 0, s, a)
     if (fmt == VX_PIXEL_RGBA32F) {
@@ -605,6 +652,7 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
         else { if (st) VX_LAUNCH(1, true, false); else VX_LAUNCH(1, false, false); }
     }
 #undef VX_LAUNCH
+    if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
     return (int)hipGetLastError();
 }
 
