@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--camera", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--flags", type=int, default=0, help="VX_FLAG_* ablation bits (diagnostics; 0 = headline)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -77,7 +78,7 @@ def main():
     noise = vx.noise_synth(0)
     scene = vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
                      noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=local)
-    frame = presets.camera_frame(cam, W, H, scale=up)
+    frame = presets.camera_frame(cam, W, H, scale=up, flags=args.flags)
     torch_stream = torch.cuda.Stream()          # a real stream: torch events and the kernels share it
     torch.cuda.set_stream(torch_stream)
     stream = torch_stream.cuda_stream

@@ -242,67 +242,102 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
     }
     if (miss || !(tlo < thi)) return 0;
     const float inv_inf = 1.0f / gmax(gmax(fabsf(d0), fabsf(d1)), fabsf(d2));
+    const int p0 = st0 > 0 ? 1 : 0, p1 = st1 > 0 ? 1 : 0, p2 = st2 > 0 ? 1 : 0;
     float tcur = tlo;
     int c0 = min(max((int)floorf(o0 + tcur * d0), -cc0), a.X - cc0 - 1);
     int c1 = min(max((int)floorf(o1 + tcur * d1), -cc1), a.Y - cc1 - 1);
     int c2 = min(max((int)floorf(o2 + tcur * d2), -cc2), a.Z - cc2 - 1);
-    float tm0 = tmax_of(c0, st0, o0, d0, iv0), tm1 = tmax_of(c1, st1, o1, d1, iv1), tm2 = tmax_of(c2, st2, o2, d2, iv2);
+    float tm0 = 0.0f, tm1 = 0.0f, tm2 = 0.0f;
+    bool stale = true;                                     // tm* are recomputed lazily after skips
     uint32_t t = texel(a, c0 + cc0, c1 + cc1, c2 + cc2);
     cnt.prim_fetch++;
     int prev = (t >> 16) & 0xff;
     int dist = t >> 24;
-    int nrec = 0;
+    // glass record kept as raw traversal state; Surf records are built after the loop
+    bool have_glass = false;
+    int gc0 = 0, gc1 = 0, gc2 = 0, gax = 0;
+    float gt = 0.0f;
+    int hit_ax = -1;                                       // >= 0: opaque surface entered across that axis
+    float tcross = 0.0f;
+    int col = 0;
     const int cap = 4 * (a.X + a.Y + a.Z);
-    for (int iter = 0; iter < cap; iter++) {
+    int iter = 0;
+    for (; iter < cap; iter++) {
         const bool skip = prev == 0 && dist >= 3;
-        bool s0 = false, s1 = false, s2 = false;
-        float tcross = 0.0f;
+        int ax = 0;
         if (skip) {
             tcur = tcur + ((float)dist - 1.5f) * inv_inf;
             c0 = (int)floorf(o0 + tcur * d0);
             c1 = (int)floorf(o1 + tcur * d1);
             c2 = (int)floorf(o2 + tcur * d2);
-            tm0 = tmax_of(c0, st0, o0, d0, iv0);
-            tm1 = tmax_of(c1, st1, o1, d1, iv1);
-            tm2 = tmax_of(c2, st2, o2, d2, iv2);
+            stale = true;
         } else {
-            s0 = tm0 <= tm1 && tm0 <= tm2;
-            s1 = !s0 && tm1 <= tm2;
-            s2 = !s0 && !s1;
+            if (stale) {
+                tm0 = tmax_of(c0, st0, o0, d0, iv0);
+                tm1 = tmax_of(c1, st1, o1, d1, iv1);
+                tm2 = tmax_of(c2, st2, o2, d2, iv2);
+                stale = false;
+            }
+            const bool s0 = tm0 <= tm1 && tm0 <= tm2;
+            const bool s1 = !s0 && tm1 <= tm2;
+            ax = s0 ? 0 : (s1 ? 1 : 2);
             tcross = s0 ? tm0 : (s1 ? tm1 : tm2);
-            if (s0) { c0 += st0; tm0 = ((float)(c0 + (st0 > 0 ? 1 : 0)) - o0) * iv0; }
-            if (s1) { c1 += st1; tm1 = ((float)(c1 + (st1 > 0 ? 1 : 0)) - o1) * iv1; }
-            if (s2) { c2 += st2; tm2 = ((float)(c2 + (st2 > 0 ? 1 : 0)) - o2) * iv2; }
+            if (s0) { c0 += st0; tm0 = ((float)(c0 + p0) - o0) * iv0; }
+            else if (s1) { c1 += st1; tm1 = ((float)(c1 + p1) - o1) * iv1; }
+            else { c2 += st2; tm2 = ((float)(c2 + p2) - o2) * iv2; }
             tcur = tcross;
         }
         const int x = c0 + cc0, y = c1 + cc1, z = c2 + cc2;
         if ((unsigned)x >= (unsigned)a.X || (unsigned)y >= (unsigned)a.Y || (unsigned)z >= (unsigned)a.Z)
-            return nrec;                                           // left the grid: sky behind
+            break;                                         // left the grid: sky behind
         t = texel(a, x, y, z);
         cnt.prim_fetch++;
         dist = t >> 24;
-        if (skip) continue;                                        // the skip cannot leave air
-        const int col = (t >> 16) & 0xff;
+        if (skip) continue;                                // the skip cannot leave air
+        col = (t >> 16) & 0xff;
         if (col != prev) {
-            Surf h;
-            h.color = col;
-            h.id = col == kGlass ? 2 : 0;
-            const int st = s0 ? st0 : (s1 ? st1 : st2);
-            h.nidx = (s0 ? 0 : (s1 ? 2 : 4)) + (st > 0 ? 1 : 0);
-            const int up = st > 0 ? 0 : 1;
-            h.c0 = x + (s0 ? up : 0);
-            h.c1 = y + (s1 ? up : 0);
-            h.c2 = z + (s2 ? up : 0);
-            h.f0 = s0 ? 0.0f : (o0 + tcross * d0) - (float)c0;
-            h.f1 = s1 ? 0.0f : (o1 + tcross * d1) - (float)c1;
-            h.f2 = s2 ? 0.0f : (o2 + tcross * d2) - (float)c2;
-            if (nrec == 0) g0 = h; else g1 = h;
-            nrec++;
-            if (h.id != 2 || nrec == 2) return nrec;
+            if (col == kGlass && !have_glass) {            // glass: blend over the next surface
+                have_glass = true;
+                gc0 = c0; gc1 = c1; gc2 = c2; gax = ax; gt = tcross;
+            } else {
+                hit_ax = ax;
+                break;
+            }
         }
         prev = col;
     }
-    cnt.cap_hit++;
+    if (iter == cap) cnt.cap_hit++;
+    // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
+    int nrec = 0;
+    if (have_glass) {
+        const int st = gax == 0 ? st0 : (gax == 1 ? st1 : st2);
+        const int up = st > 0 ? 0 : 1;
+        g0.id = 2;
+        g0.color = kGlass;
+        g0.nidx = 2 * gax + (st > 0 ? 1 : 0);
+        g0.c0 = gc0 + cc0 + (gax == 0 ? up : 0);
+        g0.c1 = gc1 + cc1 + (gax == 1 ? up : 0);
+        g0.c2 = gc2 + cc2 + (gax == 2 ? up : 0);
+        g0.f0 = gax == 0 ? 0.0f : (o0 + gt * d0) - (float)gc0;
+        g0.f1 = gax == 1 ? 0.0f : (o1 + gt * d1) - (float)gc1;
+        g0.f2 = gax == 2 ? 0.0f : (o2 + gt * d2) - (float)gc2;
+        nrec = 1;
+    }
+    if (hit_ax >= 0) {
+        Surf &h = have_glass ? g1 : g0;
+        const int st = hit_ax == 0 ? st0 : (hit_ax == 1 ? st1 : st2);
+        const int up = st > 0 ? 0 : 1;
+        h.id = col == kGlass ? 2 : 0;
+        h.color = col;
+        h.nidx = 2 * hit_ax + (st > 0 ? 1 : 0);
+        h.c0 = c0 + cc0 + (hit_ax == 0 ? up : 0);
+        h.c1 = c1 + cc1 + (hit_ax == 1 ? up : 0);
+        h.c2 = c2 + cc2 + (hit_ax == 2 ? up : 0);
+        h.f0 = hit_ax == 0 ? 0.0f : (o0 + tcross * d0) - (float)c0;
+        h.f1 = hit_ax == 1 ? 0.0f : (o1 + tcross * d1) - (float)c1;
+        h.f2 = hit_ax == 2 ? 0.0f : (o2 + tcross * d2) - (float)c2;
+        nrec++;
+    }
     return nrec;
 }
 
