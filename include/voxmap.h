@@ -49,6 +49,8 @@ extern "C" {
 #define VX_FLAG_NO_SHADOW 0x1u   /* skip the sun march (render.frag:232-235) */
 #define VX_FLAG_NO_AO 0x2u       /* skip the trilinear AO sample (render.frag:223-225) */
 #define VX_FLAG_NO_CLOUDS 0x4u   /* sky without noise fetches (render.frag:181-203) */
+#define VX_FLAG_PRIMARY_ONLY 0x8u /* primary visibility only: v_color of the first surface
+                                    (render.vert:30), sky = palette(0); BASELINE config C1 */
 
 typedef struct vx_scene vx_scene;
 

@@ -485,6 +485,12 @@ static void render_pixel(const vxo_scene *s, const vxo_frame *f, int w, int h, i
     memset(&sky, 0, sizeof sky);
     sky.id = 1;
     sky.normal_idx = 1;
+    if (f->flags & 0x8u) {   /* VX_FLAG_PRIMARY_ONLY: v_color of the first surface, sky = palette(0) */
+        if (st) { if (n == 0) st->sky_px++; else if (g[0].id == 2) st->glass_px++; else st->block_px++; }
+        palette(n == 0 ? 0 : g[0].color, out);
+        out[3] = 1.0f;
+        return;
+    }
     if (n == 0) {
         if (st) st->sky_px++;
         vxo_shade(s, f, &sky, d, out, st);

@@ -145,7 +145,7 @@ def test_tiles_and_detile_equal_full_frame(full_scene):
 
 
 @pytest.mark.parametrize("case", ["sun_axis_zero", "sun_below", "quality0", "no_shadow", "no_ao", "no_clouds",
-                                  "short_budget"])
+                                  "short_budget", "primary_only", "sun_tiny_component"])
 def test_edge_params(noise, case):
     import oracle
     import voxmap_amd as vx
@@ -168,6 +168,10 @@ def test_edge_params(noise, case):
         kw["flags"] = vx.FLAG_NO_CLOUDS
     elif case == "short_budget":
         kw["max_shadow_steps"] = 5
+    elif case == "primary_only":
+        kw["flags"] = vx.FLAG_PRIMARY_ONLY
+    elif case == "sun_tiny_component":
+        kw["sun"] = (0.8, 1e-4, 0.6)         # below the fast path's 2^-10 bound: literal march
     fr = vx.make_frame((48.0, 24.0, 18.0), (1.1, 0.0, 0.6), 128, 80, **kw)
     with _scene(vx, field, noise, dims) as sc:
         dev_field = sc.read_field()

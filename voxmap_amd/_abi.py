@@ -21,7 +21,7 @@ ERROR_NAMES = {
 
 FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB = 0, 1, 2, 3
 PIXEL_RGBA32F, PIXEL_RGBA8 = 0, 1
-FLAG_NO_SHADOW, FLAG_NO_AO, FLAG_NO_CLOUDS = 0x1, 0x2, 0x4
+FLAG_NO_SHADOW, FLAG_NO_AO, FLAG_NO_CLOUDS, FLAG_PRIMARY_ONLY = 0x1, 0x2, 0x4, 0x8
 
 
 class SceneDesc(C.Structure):

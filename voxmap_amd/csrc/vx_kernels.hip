@@ -107,8 +107,14 @@ struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
 };
 
+// Field texels through a buffer resource: 32-bit byte offsets (the largest
+// field, 3072x768x96x4 B, is < 2^32) and hardware range checking.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t field_rsrc(const KernelArgs &a) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)a.field, 0, (int)((unsigned)a.X * a.Y * a.Z * 4u), 0x00020000);
+}
 __device__ __forceinline__ uint32_t texel(const KernelArgs &a, int x, int y, int z) {
-    return a.field[(unsigned)x + (unsigned)a.X * ((unsigned)y + (unsigned)a.Y * (unsigned)z)];
+    const unsigned idx = (unsigned)x + (unsigned)a.X * ((unsigned)y + (unsigned)a.Y * (unsigned)z);
+    return __builtin_amdgcn_raw_buffer_load_b32(field_rsrc(a), idx * 4u, 0, 0);
 }
 
 // ---------------- sun march: render.frag:75-142 ----------------
@@ -280,11 +286,20 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
             }
             const bool s0 = tm0 <= tm1 && tm0 <= tm2;
             const bool s1 = !s0 && tm1 <= tm2;
+            const bool s2 = !s0 && !s1;
             ax = s0 ? 0 : (s1 ? 1 : 2);
             tcross = s0 ? tm0 : (s1 ? tm1 : tm2);
-            if (s0) { c0 += st0; tm0 = ((float)(c0 + p0) - o0) * iv0; }
-            else if (s1) { c1 += st1; tm1 = ((float)(c1 + p1) - o1) * iv1; }
-            else { c2 += st2; tm2 = ((float)(c2 + p2) - o2) * iv2; }
+            c0 += s0 ? st0 : 0;
+            c1 += s1 ? st1 : 0;
+            c2 += s2 ? st2 : 0;
+            // recompute the crossing time of the stepped axis only (selects, no branches)
+            const int cs = s0 ? c0 + p0 : (s1 ? c1 + p1 : c2 + p2);
+            const float os = s0 ? o0 : (s1 ? o1 : o2);
+            const float is = s0 ? iv0 : (s1 ? iv1 : iv2);
+            const float tn = ((float)cs - os) * is;
+            tm0 = s0 ? tn : tm0;
+            tm1 = s1 ? tn : tm1;
+            tm2 = s2 ? tn : tm2;
             tcur = tcross;
         }
         const int x = c0 + cc0, y = c1 + cc1, z = c2 + cc2;
@@ -560,7 +575,15 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
         Surf g[2];
         const int n = primary(a, d0, d1, d2, g[0], g[1], cnt);
         float rgba[4];
-        if (n == 0) {
+        if (F.flags & VX_FLAG_PRIMARY_ONLY) {
+            const int pc = n == 0 ? 0 : g[0].color;
+            rgba[0] = pc < 22 ? kPalette[pc][0] : 1.0f;
+            rgba[1] = pc < 22 ? kPalette[pc][1] : 1.0f;
+            rgba[2] = pc < 22 ? kPalette[pc][2] : 1.0f;
+            n_sky = n == 0;
+            n_glass = n != 0 && g[0].id == 2;
+            n_block = n != 0 && g[0].id != 2;
+        } else if (n == 0) {
             n_sky = 1;
             shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
