@@ -234,9 +234,14 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
  * last and blended (render.js:84-86); the surface behind a glass entry is the
  * next colour change, which is never glass, so one blend layer is exact.
  *
- * Traversal: ray/AABB entry, then a DDA over cells in camera-relative
- * coordinates; in an air cell whose A byte holds Chebyshev distance D >= 3 the
- * ray jumps (D-1.5)/|d|_inf, which cannot leave the air box around the cell.
+ * Traversal ("box-exit" stepping): from the current cell c with A-channel
+ * Chebyshev distance D (air) every cell of the box c +- (D-1) is air, so the ray
+ * jumps straight to the face where it leaves that box: per axis the crossing
+ * time of the box's far face, the earliest one (ties x, then y, then z) is the
+ * exit axis; the next cell is one past the box on that axis and floor() of the
+ * exit point, clamped into the box, on the others.  With D = 1 (or inside a
+ * non-air cell) the box is the cell itself and the step is an exact DDA step.
+ * Camera-relative cells keep the fp32 coordinates small.
  */
 static inline int in_grid(const vxo_scene *s, const int a[3]) {
     return a[0] >= 0 && a[1] >= 0 && a[2] >= 0 && a[0] < s->X && a[1] < s->Y && a[2] < s->Z;
@@ -252,7 +257,7 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
     float tlo = 0.0f, thi = INFINITY;
     *fetches = 0;
     *cap_hit = 0;
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < 3; i++) {        /* ray / grid AABB */
         stp[i] = d[i] > 0.0f ? 1 : -1;
         float lo = (float)(0 - cc[i]) - o[i];
         float hi = (float)(dims[i] - cc[i]) - o[i];
@@ -268,76 +273,61 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
         }
     }
     if (!(tlo < thi)) return 0;
-    float amax = g_max(g_max(fabsf(d[0]), fabsf(d[1])), fabsf(d[2]));
-    float inv_inf = 1.0f / amax;
 
-    int c[3];         /* camera-relative cell */
-    float tmax[3];
-    float tcur = tlo;
+    int c[3];                            /* camera-relative cell */
     for (int i = 0; i < 3; i++) {
-        float p = o[i] + tcur * d[i];
+        float p = o[i] + tlo * d[i];
         int ci = g_f2i(floorf(p));
         int lo = -cc[i], hi = dims[i] - cc[i] - 1;
         c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
     }
-    for (int i = 0; i < 3; i++)
-        tmax[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? 1 : 0)) - o[i]) * inv[i] : INFINITY;
-
-    int nrec = 0;
     int abs_c[3] = {c[0] + cc[0], c[1] + cc[1], c[2] + cc[2]};
     const uint8_t *tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
     (*fetches)++;
     int prev = tx[2];
     int dist = tx[3];
+    int nrec = 0;
     const int cap = 4 * (dims[0] + dims[1] + dims[2]);
     for (int iter = 0; iter < cap; iter++) {
-        if (prev == 0 && dist >= 3) {
-            /* Chebyshev skip inside the air box of the current cell */
-            tcur = tcur + ((float)dist - 1.5f) * inv_inf;
-            for (int i = 0; i < 3; i++) {
-                float p = o[i] + tcur * d[i];
-                c[i] = g_f2i(floorf(p));
-                tmax[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? 1 : 0)) - o[i]) * inv[i] : INFINITY;
+        const int R = (prev == 0 && dist > 0) ? dist - 1 : 0;     /* air box half-size */
+        float tb[3];
+        for (int i = 0; i < 3; i++)
+            tb[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? R + 1 : -R)) - o[i]) * inv[i] : INFINITY;
+        const int a = (tb[0] <= tb[1] && tb[0] <= tb[2]) ? 0 : (tb[1] <= tb[2] ? 1 : 2);
+        const float te = tb[a];
+        for (int i = 0; i < 3; i++) {
+            if (i == a) {
+                c[i] = c[i] + stp[i] * (R + 1);
+            } else {
+                int v = g_f2i(floorf(o[i] + te * d[i]));
+                c[i] = v < c[i] - R ? c[i] - R : (v > c[i] + R ? c[i] + R : v);
             }
-        } else {
-            int a = (tmax[0] <= tmax[1] && tmax[0] <= tmax[2]) ? 0 : (tmax[1] <= tmax[2] ? 1 : 2);
-            float tcross = tmax[a];
-            c[a] += stp[a];
-            tmax[a] = ((float)(c[a] + (stp[a] > 0 ? 1 : 0)) - o[a]) * inv[a];
-            tcur = tcross;
-            abs_c[0] = c[0] + cc[0]; abs_c[1] = c[1] + cc[1]; abs_c[2] = c[2] + cc[2];
-            if (!in_grid(s, abs_c)) return nrec;   /* left the grid: sky behind */
-            tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
-            (*fetches)++;
-            int col = tx[2];
-            dist = tx[3];
-            if (col != prev) {
-                vxo_gbuf *h = &g[nrec];
-                h->color = col;
-                h->id = col == GLASS_INDEX ? 2 : 0;
-                h->normal_idx = 2 * a + (stp[a] > 0 ? 1 : 0);
-                for (int i = 0; i < 3; i++) {
-                    if (i == a) {
-                        h->cell[i] = abs_c[i] + (stp[a] > 0 ? 0 : 1);
-                        h->fract[i] = 0.0f;
-                    } else {
-                        float p = o[i] + tcross * d[i];
-                        h->cell[i] = abs_c[i];
-                        h->fract[i] = p - (float)c[i];
-                    }
-                }
-                nrec++;
-                if (h->id != 2 || nrec == 2) return nrec;
-            }
-            prev = col;
-            continue;
         }
         abs_c[0] = c[0] + cc[0]; abs_c[1] = c[1] + cc[1]; abs_c[2] = c[2] + cc[2];
-        if (!in_grid(s, abs_c)) return nrec;
+        if (!in_grid(s, abs_c)) return nrec;   /* left the grid: sky behind */
         tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
         (*fetches)++;
+        const int col = tx[2];
         dist = tx[3];
-        /* prev stays 0: the skip cannot leave air */
+        if (col != prev) {
+            vxo_gbuf *h = &g[nrec];
+            h->color = col;
+            h->id = col == GLASS_INDEX ? 2 : 0;
+            h->normal_idx = 2 * a + (stp[a] > 0 ? 1 : 0);
+            for (int i = 0; i < 3; i++) {
+                if (i == a) {
+                    h->cell[i] = abs_c[i] + (stp[a] > 0 ? 0 : 1);
+                    h->fract[i] = 0.0f;
+                } else {
+                    float p = o[i] + te * d[i];
+                    h->cell[i] = abs_c[i];
+                    h->fract[i] = p - (float)c[i];
+                }
+            }
+            nrec++;
+            if (h->id != 2 || nrec == 2) return nrec;
+        }
+        prev = col;
     }
     *cap_hit = 1;
     return nrec;

@@ -204,13 +204,12 @@ __device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float
 
 // ---------------- primary visibility ----------------
 // First in-grid colour change along the view ray = the nearest front face of
-// the greedy mesh of sdf.cpp:281-356 after back-face culling; in air cells
-// with Chebyshev distance D >= 3 (A byte) the ray jumps (D-1.5)/|d|_inf.
-// Camera-relative cells; returns 0 sky, 1 surface, 2 glass + what is behind.
-__device__ __forceinline__ float tmax_of(int c, int st, float o, float d, float iv) {
-    return d != 0.0f ? ((float)(c + (st > 0 ? 1 : 0)) - o) * iv : kInf;
-}
-
+// the greedy mesh of sdf.cpp:281-356 after back-face culling.  Box-exit
+// stepping (oracle/vxo_render.c vxo_primary): the A byte D of an air cell
+// says the box c +- (D-1) is air, so one step goes to the face where the ray
+// leaves that box (D = 1 or a non-air cell: an exact DDA step).  The loop body
+// is branch-free except for the exits.  Camera-relative cells; returns 0 sky,
+// 1 surface, 2 glass + what is behind.
 __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &g0, Surf &g1, Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
@@ -247,73 +246,50 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
         } else miss |= !(lo <= 0.0f && 0.0f < hi);
     }
     if (miss || !(tlo < thi)) return 0;
-    const float inv_inf = 1.0f / gmax(gmax(fabsf(d0), fabsf(d1)), fabsf(d2));
-    const int p0 = st0 > 0 ? 1 : 0, p1 = st1 > 0 ? 1 : 0, p2 = st2 > 0 ? 1 : 0;
-    float tcur = tlo;
-    int c0 = min(max((int)floorf(o0 + tcur * d0), -cc0), a.X - cc0 - 1);
-    int c1 = min(max((int)floorf(o1 + tcur * d1), -cc1), a.Y - cc1 - 1);
-    int c2 = min(max((int)floorf(o2 + tcur * d2), -cc2), a.Z - cc2 - 1);
-    float tm0 = 0.0f, tm1 = 0.0f, tm2 = 0.0f;
-    bool stale = true;                                     // tm* are recomputed lazily after skips
+    // far-face offsets of the box: +R+1 for a positive step, -R for a negative one
+    const bool z0 = d0 == 0.0f, z1 = d1 == 0.0f, z2 = d2 == 0.0f;
+    int c0 = min(max((int)floorf(o0 + tlo * d0), -cc0), a.X - cc0 - 1);
+    int c1 = min(max((int)floorf(o1 + tlo * d1), -cc1), a.Y - cc1 - 1);
+    int c2 = min(max((int)floorf(o2 + tlo * d2), -cc2), a.Z - cc2 - 1);
     uint32_t t = texel(a, c0 + cc0, c1 + cc1, c2 + cc2);
     cnt.prim_fetch++;
     int prev = (t >> 16) & 0xff;
     int dist = t >> 24;
-    // glass record kept as raw traversal state; Surf records are built after the loop
     bool have_glass = false;
     int gc0 = 0, gc1 = 0, gc2 = 0, gax = 0;
     float gt = 0.0f;
-    int hit_ax = -1;                                       // >= 0: opaque surface entered across that axis
-    float tcross = 0.0f;
-    int col = 0;
+    int hit_ax = -1;
+    float te = 0.0f;
+    int ax = 0, col = 0;
     const int cap = 4 * (a.X + a.Y + a.Z);
     int iter = 0;
     for (; iter < cap; iter++) {
-        const bool skip = prev == 0 && dist >= 3;
-        int ax = 0;
-        if (skip) {
-            tcur = tcur + ((float)dist - 1.5f) * inv_inf;
-            c0 = (int)floorf(o0 + tcur * d0);
-            c1 = (int)floorf(o1 + tcur * d1);
-            c2 = (int)floorf(o2 + tcur * d2);
-            stale = true;
-        } else {
-            if (stale) {
-                tm0 = tmax_of(c0, st0, o0, d0, iv0);
-                tm1 = tmax_of(c1, st1, o1, d1, iv1);
-                tm2 = tmax_of(c2, st2, o2, d2, iv2);
-                stale = false;
-            }
-            const bool s0 = tm0 <= tm1 && tm0 <= tm2;
-            const bool s1 = !s0 && tm1 <= tm2;
-            const bool s2 = !s0 && !s1;
-            ax = s0 ? 0 : (s1 ? 1 : 2);
-            tcross = s0 ? tm0 : (s1 ? tm1 : tm2);
-            c0 += s0 ? st0 : 0;
-            c1 += s1 ? st1 : 0;
-            c2 += s2 ? st2 : 0;
-            // recompute the crossing time of the stepped axis only (selects, no branches)
-            const int cs = s0 ? c0 + p0 : (s1 ? c1 + p1 : c2 + p2);
-            const float os = s0 ? o0 : (s1 ? o1 : o2);
-            const float is = s0 ? iv0 : (s1 ? iv1 : iv2);
-            const float tn = ((float)cs - os) * is;
-            tm0 = s0 ? tn : tm0;
-            tm1 = s1 ? tn : tm1;
-            tm2 = s2 ? tn : tm2;
-            tcur = tcross;
-        }
+        const int R = (prev == 0 && dist > 0) ? dist - 1 : 0;
+        const float tb0 = z0 ? kInf : ((float)(c0 + (st0 > 0 ? R + 1 : -R)) - o0) * iv0;
+        const float tb1 = z1 ? kInf : ((float)(c1 + (st1 > 0 ? R + 1 : -R)) - o1) * iv1;
+        const float tb2 = z2 ? kInf : ((float)(c2 + (st2 > 0 ? R + 1 : -R)) - o2) * iv2;
+        const bool s0 = tb0 <= tb1 && tb0 <= tb2;
+        const bool s1 = !s0 && tb1 <= tb2;
+        const bool s2 = !s0 && !s1;
+        te = s0 ? tb0 : (s1 ? tb1 : tb2);
+        ax = s0 ? 0 : (s1 ? 1 : 2);
+        const int w0 = min(max((int)floorf(o0 + te * d0), c0 - R), c0 + R);
+        const int w1 = min(max((int)floorf(o1 + te * d1), c1 - R), c1 + R);
+        const int w2 = min(max((int)floorf(o2 + te * d2), c2 - R), c2 + R);
+        c0 = s0 ? c0 + st0 * (R + 1) : w0;
+        c1 = s1 ? c1 + st1 * (R + 1) : w1;
+        c2 = s2 ? c2 + st2 * (R + 1) : w2;
         const int x = c0 + cc0, y = c1 + cc1, z = c2 + cc2;
         if ((unsigned)x >= (unsigned)a.X || (unsigned)y >= (unsigned)a.Y || (unsigned)z >= (unsigned)a.Z)
             break;                                         // left the grid: sky behind
         t = texel(a, x, y, z);
         cnt.prim_fetch++;
         dist = t >> 24;
-        if (skip) continue;                                // the skip cannot leave air
         col = (t >> 16) & 0xff;
         if (col != prev) {
             if (col == kGlass && !have_glass) {            // glass: blend over the next surface
                 have_glass = true;
-                gc0 = c0; gc1 = c1; gc2 = c2; gax = ax; gt = tcross;
+                gc0 = c0; gc1 = c1; gc2 = c2; gax = ax; gt = te;
             } else {
                 hit_ax = ax;
                 break;
@@ -348,9 +324,9 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
         h.c0 = c0 + cc0 + (hit_ax == 0 ? up : 0);
         h.c1 = c1 + cc1 + (hit_ax == 1 ? up : 0);
         h.c2 = c2 + cc2 + (hit_ax == 2 ? up : 0);
-        h.f0 = hit_ax == 0 ? 0.0f : (o0 + tcross * d0) - (float)c0;
-        h.f1 = hit_ax == 1 ? 0.0f : (o1 + tcross * d1) - (float)c1;
-        h.f2 = hit_ax == 2 ? 0.0f : (o2 + tcross * d2) - (float)c2;
+        h.f0 = hit_ax == 0 ? 0.0f : (o0 + te * d0) - (float)c0;
+        h.f1 = hit_ax == 1 ? 0.0f : (o1 + te * d1) - (float)c1;
+        h.f2 = hit_ax == 2 ? 0.0f : (o2 + te * d2) - (float)c2;
         nrec++;
     }
     return nrec;
