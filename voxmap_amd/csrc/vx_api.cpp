@@ -103,6 +103,8 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     const int NW = d->noise_w ? d->noise_w : 1024, NH = d->noise_h ? d->noise_h : 1024;
     if (X <= 0 || Y <= 0 || Z <= 0 || X > 65535 || Y > 65535 || Z > 255)
         return set_error(VX_EINVAL, "vx_scene_create: dims out of range");
+    if ((unsigned long long)X * Y * Z * 4ull >= (1ull << 31))   // 32-bit buffer byte offsets in the kernels
+        return set_error(VX_EINVAL, "vx_scene_create: field larger than 2 GiB");
     if ((NW & (NW - 1)) || (NH & (NH - 1))) return set_error(VX_EINVAL, "noise dims must be powers of two");
     if (!!d->map_path == !!d->map_bytes) return set_error(VX_EINVAL, "set exactly one of map_path / map_bytes");
     const int cap = d->dist_cap ? d->dist_cap : 32;

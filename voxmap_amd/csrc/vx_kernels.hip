@@ -112,8 +112,10 @@ struct Counters {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t field_rsrc(const KernelArgs &a) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)a.field, 0, (int)((unsigned)a.X * a.Y * a.Z * 4u), 0x00020000);
 }
+// x + X*(y + Y*z): every operand < 2^24 for the grids we accept (<= 65535 x
+// 65535 x 255 with X*Y*Z*4 < 2^32), so two full-rate v_mad_u32_u24.
 __device__ __forceinline__ uint32_t texel(const KernelArgs &a, int x, int y, int z) {
-    const unsigned idx = (unsigned)x + (unsigned)a.X * ((unsigned)y + (unsigned)a.Y * (unsigned)z);
+    const unsigned idx = (unsigned)x + __umul24((unsigned)a.X, (unsigned)y + __umul24((unsigned)a.Y, (unsigned)z));
     return __builtin_amdgcn_raw_buffer_load_b32(field_rsrc(a), idx * 4u, 0, 0);
 }
 
