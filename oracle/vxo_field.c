@@ -17,8 +17,10 @@
  * The reference C++ itself is NOT compiled (SURVEY.md §8c permission denial);
  * this is a from-text restatement.
  *
- * vxo_field_dist: the build's own A-channel contents: capped
- * Chebyshev distance from each cell to the nearest non-air cell.
+ * vxo_field_dist: the build's own A-channel contents: the
+ * half-size R of the all-air box around each cell, R = D - 1 for the capped
+ * Chebyshev distance D >= 1 to the nearest non-air cell, 0 for non-air cells
+ * (so A <= cap - 1 <= 254; 255 is free for the kernels' out-of-grid sentinel).
  */
 #include "vxo.h"
 #include <stdlib.h>
@@ -148,7 +150,8 @@ void vxo_field_dist(uint8_t *rgba, int X, int Y, int Z, int cap) {
                     int m = v > ak ? v : ak;
                     if (m < best) best = m;
                 }
-                rgba[4 * ((size_t)x + (size_t)X * ((size_t)y + (size_t)Y * z)) + 3] = (unsigned char)best;
+                rgba[4 * ((size_t)x + (size_t)X * ((size_t)y + (size_t)Y * z)) + 3] =
+                    (unsigned char)(best > 0 ? best - 1 : 0);
             }
     free(g1);
     free(g2);

@@ -235,12 +235,12 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
  * next colour change, which is never glass, so one blend layer is exact.
  *
  * Traversal ("box-exit" stepping): from the current cell c with A-channel
- * Chebyshev distance D (air) every cell of the box c +- (D-1) is air, so the ray
+ * box half-size R (vxo_field_dist) every cell of the box c +- R is air, so the ray
  * jumps straight to the face where it leaves that box: per axis the crossing
  * time of the box's far face, the earliest one (ties x, then y, then z) is the
  * exit axis; the next cell is one past the box on that axis and floor() of the
- * exit point, clamped into the box, on the others.  With D = 1 (or inside a
- * non-air cell) the box is the cell itself and the step is an exact DDA step.
+ * exit point, clamped into the box, on the others.  With R = 0 (next to or
+ * inside a non-air cell) the box is the cell itself and the step is an exact DDA step.
  * Camera-relative cells keep the fp32 coordinates small.
  */
 static inline int in_grid(const vxo_scene *s, const int a[3]) {
@@ -285,11 +285,10 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
     const uint8_t *tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
     (*fetches)++;
     int prev = tx[2];
-    int dist = tx[3];
+    int R = tx[3];
     int nrec = 0;
     const int cap = 4 * (dims[0] + dims[1] + dims[2]);
     for (int iter = 0; iter < cap; iter++) {
-        const int R = (prev == 0 && dist > 0) ? dist - 1 : 0;     /* air box half-size */
         float tb[3];
         for (int i = 0; i < 3; i++)
             tb[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? R + 1 : -R)) - o[i]) * inv[i] : INFINITY;
@@ -308,7 +307,7 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
         tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
         (*fetches)++;
         const int col = tx[2];
-        dist = tx[3];
+        R = tx[3];                                 /* air box half-size */
         if (col != prev) {
             vxo_gbuf *h = &g[nrec];
             h->color = col;

@@ -248,3 +248,22 @@ def test_primary_glass_then_behind_and_boundary_rule(O):
     d2 = np.array([-1.0, 0.001, 0.002])
     n2, gb2, _, _ = o.primary(fr2.params, d2)
     assert n2 == 1 and gb2[0].color == 0 and gb2[0].normal_idx == 0 and gb2[0].cell[0] == 31
+
+
+def test_field_dist_is_air_box_half_size(O):
+    """A channel = R with the box c +- R all air and R + 1 <= cap: brute force
+    Chebyshev distance D to the nearest non-air cell (grid-bounded), R = D - 1."""
+    rng = np.random.default_rng(3)
+    Z, Y, X, cap = 9, 11, 13, 4
+    col = np.where(rng.random((Z, Y, X)) < 0.04, 7, 0).astype(np.uint8)
+    field = np.zeros((Z, Y, X, 4), np.uint8)
+    field[..., 2] = col
+    got = O.field_dist(field, cap)
+    assert np.array_equal(got[..., :3], field[..., :3])
+    solid = np.argwhere(col != 0)
+    zz, yy, xx = np.meshgrid(np.arange(Z), np.arange(Y), np.arange(X), indexing="ij")
+    D = np.full((Z, Y, X), cap)
+    for z, y, x in solid:
+        D = np.minimum(D, np.maximum(np.maximum(abs(zz - z), abs(yy - y)), abs(xx - x)))
+    assert np.array_equal(got[..., 3], np.maximum(D - 1, 0).astype(np.uint8))
+    assert got[..., 3].max() <= cap - 1           # 255 stays free for the out-of-grid sentinel

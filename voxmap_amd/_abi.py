@@ -11,6 +11,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvoxmap_hip.so")
+if os.environ.get("VOXMAP_LIB"):          # experiment variants (voxmap_amd/build.py out=...)
+    LIB_PATH = os.environ["VOXMAP_LIB"]
 
 VX_OK = 0
 VX_EINVAL, VX_EIO, VX_EFORMAT, VX_ECRYPTO, VX_ESIZE, VX_EDEVICE, VX_ENOMEM = -1, -2, -3, -4, -5, -6, -7

@@ -35,16 +35,20 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = True, out: str | None = None, defines=()) -> str:
+    """Build the library.  ``out``/``defines`` make experiment variants (A/B runs
+    select one with VOXMAP_LIB=path); the product is always the default build."""
+    target = out or OUT
+    if out is None and not defines and not force and not needs_build():
         return OUT
-    tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-shared", "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES], *LIBS]
+    tmp = target + ".tmp"
+    cmd = [hipcc(), *FLAGS, *[f"-D{d}" for d in defines], "-shared", "-o", tmp,
+           *[os.path.join(CSRC, s) for s in SOURCES], *LIBS]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

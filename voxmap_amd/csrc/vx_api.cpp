@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
@@ -49,6 +50,7 @@ struct vx_scene {
     std::vector<int> h_tiles, h_detile;   // last lists uploaded to d_tiles / d_detile
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    FieldLayout L;  // d_field is padded (vx_internal.h)
 };
 
 #define VX_HIP(call)                                                                                 \
@@ -103,12 +105,14 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     const int NW = d->noise_w ? d->noise_w : 1024, NH = d->noise_h ? d->noise_h : 1024;
     if (X <= 0 || Y <= 0 || Z <= 0 || X > 65535 || Y > 65535 || Z > 255)
         return set_error(VX_EINVAL, "vx_scene_create: dims out of range");
-    if ((unsigned long long)X * Y * Z * 4ull >= (1ull << 31))   // 32-bit buffer byte offsets in the kernels
-        return set_error(VX_EINVAL, "vx_scene_create: field larger than 2 GiB");
-    if ((NW & (NW - 1)) || (NH & (NH - 1))) return set_error(VX_EINVAL, "noise dims must be powers of two");
-    if (!!d->map_path == !!d->map_bytes) return set_error(VX_EINVAL, "set exactly one of map_path / map_bytes");
     const int cap = d->dist_cap ? d->dist_cap : 32;
     if (cap < 1 || cap > 255) return set_error(VX_EINVAL, "dist_cap must be in [1,255]");
+    const FieldLayout L = field_layout(X, Y, Z, cap);
+    // 32-bit buffer byte offsets and 24-bit index products in the kernels
+    if (L.texels * 4ull >= (1ull << 31) || (unsigned long long)L.Xp * L.Yp >= (1ull << 23))
+        return set_error(VX_EINVAL, "vx_scene_create: field too large (padded field must be < 2 GiB)");
+    if ((NW & (NW - 1)) || (NH & (NH - 1))) return set_error(VX_EINVAL, "noise dims must be powers of two");
+    if (!!d->map_path == !!d->map_bytes) return set_error(VX_EINVAL, "set exactly one of map_path / map_bytes");
     const size_t field_bytes = (size_t)X * Y * Z * 4, noise_bytes = (size_t)NW * NH * 4;
 
     std::vector<unsigned char> field, noise;
@@ -152,6 +156,18 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     if (lrc != 0 || e != hipSuccess)
         return fail(set_error(VX_EDEVICE, std::string("field distance pass failed: ") +
                                               hipGetErrorString(lrc ? (hipError_t)lrc : e)));
+    // into the padded layout the kernels read (border = out-of-grid sentinel)
+    uint32_t *padded = nullptr;
+    if ((e = hipMalloc(&padded, L.texels * 4)) != hipSuccess ||
+        (e = hipMemsetD32Async((hipDeviceptr_t)padded, 0xFF000000u, L.texels, s->stream)) != hipSuccess ||
+        (e = (hipError_t)launch_field_pad(s->d_field, padded, X, Y, Z, L.pad, 1, s->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
+        if (padded) (void)hipFree(padded);
+        return fail(set_error(VX_EDEVICE, std::string("field padding failed: ") + hipGetErrorString(e)));
+    }
+    (void)hipFree(s->d_field);
+    s->d_field = padded;
+    s->L = L;
     *out = s;
     return VX_OK;
 }
@@ -182,8 +198,13 @@ int vx_scene_read_field(vx_scene *s, void *host_out, size_t cap) {
     const size_t n = (size_t)s->X * s->Y * s->Z * 4;
     if (cap < n) return set_error(VX_EINVAL, "vx_scene_read_field: buffer too small");
     VX_HIP(hipSetDevice(s->device));
-    VX_HIP(hipMemcpyAsync(host_out, s->d_field, n, hipMemcpyDeviceToHost, s->stream));
-    VX_HIP(hipStreamSynchronize(s->stream));
+    uint32_t *lin = nullptr;
+    VX_HIP(hipMalloc(&lin, n));
+    hipError_t e = (hipError_t)launch_field_pad(s->d_field, lin, s->X, s->Y, s->Z, s->L.pad, 0, s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(host_out, lin, n, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(lin);
+    if (e != hipSuccess) return set_error(VX_EDEVICE, std::string("vx_scene_read_field: ") + hipGetErrorString(e));
     return VX_OK;
 }
 
@@ -195,6 +216,14 @@ static int check_params(const vx_scene *s, const vx_frame_params *p, int w, int 
         if (!std::isfinite(p->cam_fract[i]) || !std::isfinite(p->ray_fwd[i]) || !std::isfinite(p->ray_right[i]) ||
             !std::isfinite(p->ray_up[i]) || !std::isfinite(p->sun_dir[i]))
             return set_error(VX_EINVAL, "non-finite frame parameter");
+    // u_fractPos is fract(position) (render.js:289-290); the primary traversal
+    // relies on 0 <= o < 1 and on camera-relative cells below 2^22
+    for (int i = 0; i < 3; i++) {
+        if (!(p->cam_fract[i] >= 0.0f && p->cam_fract[i] < 1.0f))
+            return set_error(VX_EINVAL, "cam_fract must be in [0, 1)");
+        if (p->cam_cell[i] <= -(1 << 22) || p->cam_cell[i] >= (1 << 22))
+            return set_error(VX_EINVAL, "cam_cell out of range (|cell| < 2^22)");
+    }
     return VX_OK;
 }
 
@@ -234,6 +263,13 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.p = *p;
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
+    a.Xp = s->L.Xp;
+    a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
+    a.k0 = (unsigned)s->L.k0;
+    a.texels = (unsigned)s->L.texels;
+    a.kcam = (unsigned)(p->cam_cell[0] + s->L.pad) + (unsigned)a.Xp * (unsigned)(p->cam_cell[1] + s->L.pad) +
+             a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);   // mod 2^32
+
     if (stats) {
         a.stats = s->d_stats;
         VX_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(unsigned long long) * ST_COUNT * 64, st));
@@ -353,6 +389,10 @@ static void set_cam(const double pos[3], vx_frame_params *p) {
         const double fl = std::floor(pos[i]);
         p->cam_cell[i] = (int)fl;               // render.js:289 position.map(floor)
         p->cam_fract[i] = (float)(pos[i] - fl); // render.js:290 position.map(fract)
+        if (p->cam_fract[i] >= 1.0f) {          // fract within 2^-25 of 1 rounds up in fp32:
+            p->cam_cell[i] += 1;                // the same point as cell + 1, fract 0
+            p->cam_fract[i] = 0.0f;
+        }
     }
 }
 

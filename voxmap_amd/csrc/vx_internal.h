@@ -37,7 +37,7 @@ struct FrameConsts {
 
 // Parameters of one render launch (passed by value to the kernel).
 struct KernelArgs {
-    const uint32_t *field;   // RGBA8 texels, x fastest (render.js:62)
+    const uint32_t *field;   // RGBA8 texels, x fastest (render.js:62), padded (FieldLayout)
     const uint32_t *noise;   // RGBA8 noise texels
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
@@ -50,6 +50,11 @@ struct KernelArgs {
     unsigned long long *stats;   // device counters (nullptr = no stats)
     vx_frame_params p;
     int max_shadow_steps;
+    int Xp;                  // padded row length (FieldLayout)
+    unsigned XpYp;           // padded slice size
+    unsigned k0;             // padded index of grid cell (0, 0, 0)
+    unsigned texels;         // padded texel count
+    unsigned kcam;           // padded index of the camera cell, mod 2^32
     FrameConsts fc;
 };
 
@@ -59,6 +64,17 @@ enum StatSlot {
     ST_PIXELS = 0, ST_SKY, ST_BLOCK, ST_GLASS, ST_PRIM_FETCH, ST_SHADOW_RAYS, ST_SHADOW_FETCH,
     ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_COUNT
 };
+
+// Field layout in HBM: the X x Y x Z grid (x fastest, as map.bin) inside a
+// border of pad = cap sentinel texels on every side.
+struct FieldLayout {
+    int pad, Xp, Yp, Zp;
+    size_t texels;           // Xp * Yp * Zp
+    size_t k0;               // index of grid cell (0, 0, 0)
+};
+FieldLayout field_layout(int X, int Y, int Z, int cap);
+// linear grid <-> padded field; to_padded = 1 scatters src into dst
+int launch_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, int pad, int to_padded, void *stream);
 
 // Launchers (vx_kernels.hip).  Return a hipError_t as int.
 int launch_render(const KernelArgs &a, int pixel_format, void *stream);

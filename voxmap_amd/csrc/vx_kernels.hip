@@ -107,15 +107,24 @@ struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
 };
 
-// Field texels through a buffer resource: 32-bit byte offsets (the largest
-// field, 3072x768x96x4 B, is < 2^32) and hardware range checking.
+// Field in HBM: the reference's x-fastest texels inside a border of P = cap
+// sentinel cells (A = 255, never a real value: A <= cap - 1 <= 254), so the
+// primary traversal detects leaving the grid from the texel it loads.  Texels
+// go through buffer resources: 32-bit byte offsets (fields are < 2 GiB) and
+// hardware range checking (out-of-range reads return 0).
+constexpr uint32_t kSentinel = 0xFF000000u;
+
+// grid-origin based: texel (x, y, z) of the unpadded grid at x + Xp*y + XpYp*z
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t field_rsrc(const KernelArgs &a) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)a.field, 0, (int)((unsigned)a.X * a.Y * a.Z * 4u), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(a.field + a.k0), 0, (int)((a.texels - a.k0) * 4u), 0x00020000);
 }
-// x + X*(y + Y*z): every operand < 2^24 for the grids we accept (<= 65535 x
-// 65535 x 255 with X*Y*Z*4 < 2^32), so two full-rate v_mad_u32_u24.
+// buffer-start based (primary traversal: padded indices)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t field_rsrc_padded(const KernelArgs &a) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)a.field, 0, (int)(a.texels * 4u), 0x00020000);
+}
+// Xp < 2^16 and XpYp < 2^23 (vx_scene_create), so full-rate 24-bit multiplies.
 __device__ __forceinline__ uint32_t texel(const KernelArgs &a, int x, int y, int z) {
-    const unsigned idx = (unsigned)x + __umul24((unsigned)a.X, (unsigned)y + __umul24((unsigned)a.Y, (unsigned)z));
+    const unsigned idx = (unsigned)x + __umul24((unsigned)a.Xp, (unsigned)y) + __umul24(a.XpYp, (unsigned)z);
     return __builtin_amdgcn_raw_buffer_load_b32(field_rsrc(a), idx * 4u, 0, 0);
 }
 
@@ -207,128 +216,147 @@ __device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float
 // ---------------- primary visibility ----------------
 // First in-grid colour change along the view ray = the nearest front face of
 // the greedy mesh of sdf.cpp:281-356 after back-face culling.  Box-exit
-// stepping (oracle/vxo_render.c vxo_primary): the A byte D of an air cell
-// says the box c +- (D-1) is air, so one step goes to the face where the ray
-// leaves that box (D = 1 or a non-air cell: an exact DDA step).  The loop body
-// is branch-free except for the exits.  Camera-relative cells; returns 0 sky,
-// 1 surface, 2 glass + what is behind.
+// stepping (oracle/vxo_render.c vxo_primary): the A byte R of a cell says the
+// box c +- R is air, so one step goes to the face where the ray leaves that
+// box (R = 0: an exact DDA step).  Returns 0 sky, 1 surface, 2 glass + what
+// is behind.
+//
+// The loop runs on camera-relative cells held as fp32 integers (exact: the
+// host keeps |cam_cell| < 2^22), with x and y in packed-fp32 pairs:
+//   h = c + hp (hp = 1 on a positive axis, 0 on a negative one), s = +-1;
+//   far face    A  = c + (s > 0 ? R + 1 : -R) = fma(s, R, h)       (exact)
+//   crossing    tb = (A - o) * iv                                   (= oracle)
+//   exit axis   next h = A + s; others med3(floor(o + te*d) + hp, h - R, h + R)
+// d == 0 is a positive axis with iv = +inf: A - o >= 1 - o > 0 (0 <= o < 1 is
+// checked by vx_render), so tb = +inf exactly as the oracle's.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &g0, Surf &g1, Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
     const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
-    const int st0 = d0 > 0.0f ? 1 : -1, st1 = d1 > 0.0f ? 1 : -1, st2 = d2 > 0.0f ? 1 : -1;
     float tlo = 0.0f, thi = kInf;
-    float iv0 = 0.0f, iv1 = 0.0f, iv2 = 0.0f;
+    float iv0 = kInf, iv1 = kInf, iv2 = kInf;
     bool miss = false;
-    {
-        const float lo = (float)(0 - cc0) - o0, hi = (float)(a.X - cc0) - o0;
-        if (d0 != 0.0f) {
-            iv0 = 1.0f / d0;
-            float t0 = lo * iv0, t1 = hi * iv0;
-            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
-            tlo = gmax(tlo, t0); thi = gmin(thi, t1);
-        } else miss |= !(lo <= 0.0f && 0.0f < hi);
+#define VX_SLAB(D, IV, CC, O, DIM)                                          \
+    {                                                                         \
+        const float lo = (float)(0 - CC) - O, hi = (float)(DIM - CC) - O;     \
+        if (D != 0.0f) {                                                      \
+            IV = 1.0f / D;                                                    \
+            float t0 = lo * IV, t1 = hi * IV;                                 \
+            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }           \
+            tlo = gmax(tlo, t0); thi = gmin(thi, t1);                         \
+        } else miss |= !(lo <= 0.0f && 0.0f < hi);                            \
     }
-    {
-        const float lo = (float)(0 - cc1) - o1, hi = (float)(a.Y - cc1) - o1;
-        if (d1 != 0.0f) {
-            iv1 = 1.0f / d1;
-            float t0 = lo * iv1, t1 = hi * iv1;
-            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
-            tlo = gmax(tlo, t0); thi = gmin(thi, t1);
-        } else miss |= !(lo <= 0.0f && 0.0f < hi);
-    }
-    {
-        const float lo = (float)(0 - cc2) - o2, hi = (float)(a.Z - cc2) - o2;
-        if (d2 != 0.0f) {
-            iv2 = 1.0f / d2;
-            float t0 = lo * iv2, t1 = hi * iv2;
-            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
-            tlo = gmax(tlo, t0); thi = gmin(thi, t1);
-        } else miss |= !(lo <= 0.0f && 0.0f < hi);
-    }
+    VX_SLAB(d0, iv0, cc0, o0, a.X)
+    VX_SLAB(d1, iv1, cc1, o1, a.Y)
+    VX_SLAB(d2, iv2, cc2, o2, a.Z)
+#undef VX_SLAB
     if (miss || !(tlo < thi)) return 0;
-    // far-face offsets of the box: +R+1 for a positive step, -R for a negative one
-    const bool z0 = d0 == 0.0f, z1 = d1 == 0.0f, z2 = d2 == 0.0f;
-    int c0 = min(max((int)floorf(o0 + tlo * d0), -cc0), a.X - cc0 - 1);
-    int c1 = min(max((int)floorf(o1 + tlo * d1), -cc1), a.Y - cc1 - 1);
-    int c2 = min(max((int)floorf(o2 + tlo * d2), -cc2), a.Z - cc2 - 1);
-    uint32_t t = texel(a, c0 + cc0, c1 + cc1, c2 + cc2);
+    const int c0 = min(max((int)floorf(o0 + tlo * d0), -cc0), a.X - cc0 - 1);
+    const int c1 = min(max((int)floorf(o1 + tlo * d1), -cc1), a.Y - cc1 - 1);
+    const int c2 = min(max((int)floorf(o2 + tlo * d2), -cc2), a.Z - cc2 - 1);
+    const bool p0 = !(d0 < 0.0f), p1 = !(d1 < 0.0f), p2 = !(d2 < 0.0f);
+    const int ip0 = p0, ip1 = p1, ip2 = p2;
+    const f2 sxy = {p0 ? 1.0f : -1.0f, p1 ? 1.0f : -1.0f};
+    const float sz = p2 ? 1.0f : -1.0f;
+    const f2 hpxy = {(float)ip0, (float)ip1};
+    const float hpz = (float)ip2;
+    const f2 oxy = {o0, o1}, dxy = {d0, d1}, ivxy = {iv0, iv1};
+    f2 hxy = {(float)(c0 + ip0), (float)(c1 + ip1)};
+    float hz = (float)(c2 + ip2);
+    // padded index of h: kray + hx + Xp*hy + XpYp*hz, mod 2^32 with 24-bit
+    // signed products (|h| < 2^23)
+    const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
+    const __amdgpu_buffer_rsrc_t rs = field_rsrc_padded(a);
+    auto fetch = [&](float x, float y, float z) -> uint32_t {
+        const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)idx * 4u, 0, 0);
+    };
+    uint32_t t = fetch(hxy.x, hxy.y, hz);
     cnt.prim_fetch++;
     int prev = (t >> 16) & 0xff;
-    int dist = t >> 24;
-    bool have_glass = false;
-    int gc0 = 0, gc1 = 0, gc2 = 0, gax = 0;
-    float gt = 0.0f;
-    int hit_ax = -1;
-    float te = 0.0f;
-    int ax = 0, col = 0;
+    float R = (float)(t >> 24);
+    bool have_glass = false, hit = false;
+    f2 gxy = {0.0f, 0.0f};
+    float gz = 0.0f, gt = 0.0f, te = 0.0f;
+    int gax = 0, hax = 0, col = 0;
     const int cap = 4 * (a.X + a.Y + a.Z);
     int iter = 0;
     for (; iter < cap; iter++) {
-        const int R = (prev == 0 && dist > 0) ? dist - 1 : 0;
-        const float tb0 = z0 ? kInf : ((float)(c0 + (st0 > 0 ? R + 1 : -R)) - o0) * iv0;
-        const float tb1 = z1 ? kInf : ((float)(c1 + (st1 > 0 ? R + 1 : -R)) - o1) * iv1;
-        const float tb2 = z2 ? kInf : ((float)(c2 + (st2 > 0 ? R + 1 : -R)) - o2) * iv2;
-        const bool s0 = tb0 <= tb1 && tb0 <= tb2;
-        const bool s1 = !s0 && tb1 <= tb2;
-        const bool s2 = !s0 && !s1;
-        te = s0 ? tb0 : (s1 ? tb1 : tb2);
-        ax = s0 ? 0 : (s1 ? 1 : 2);
-        const int w0 = min(max((int)floorf(o0 + te * d0), c0 - R), c0 + R);
-        const int w1 = min(max((int)floorf(o1 + te * d1), c1 - R), c1 + R);
-        const int w2 = min(max((int)floorf(o2 + te * d2), c2 - R), c2 + R);
-        c0 = s0 ? c0 + st0 * (R + 1) : w0;
-        c1 = s1 ? c1 + st1 * (R + 1) : w1;
-        c2 = s2 ? c2 + st2 * (R + 1) : w2;
-        const int x = c0 + cc0, y = c1 + cc1, z = c2 + cc2;
-        if ((unsigned)x >= (unsigned)a.X || (unsigned)y >= (unsigned)a.Y || (unsigned)z >= (unsigned)a.Z)
-            break;                                         // left the grid: sky behind
-        t = texel(a, x, y, z);
+        const f2 Rv = {R, R};
+        const f2 Axy = __builtin_elementwise_fma(sxy, Rv, hxy);
+        const float Az = __builtin_fmaf(sz, R, hz);
+        const f2 tbxy = (Axy - oxy) * ivxy;
+        const float tbz = (Az - o2) * iv2;
+        te = __builtin_fminf(__builtin_fminf(tbxy.x, tbxy.y), tbz);
+        const bool e0 = tbxy.x == te;
+        const bool e1 = !e0 && tbxy.y == te;
+        const bool e2 = !e0 && !e1;
+        const f2 tev = {te, te};
+        const f2 pxy = oxy + tev * dxy;
+        const float pz = o2 + te * d2;
+        const f2 fxy = {floorf(pxy.x), floorf(pxy.y)};
+        const f2 qxy = fxy + hpxy;
+        const float qz = floorf(pz) + hpz;
+        const f2 loxy = hxy - Rv, hixy = hxy + Rv;
+        const f2 xxy = Axy + sxy;
+        const float xz = Az + sz;
+        const float n0 = e0 ? xxy.x : __builtin_amdgcn_fmed3f(qxy.x, loxy.x, hixy.x);
+        const float n1 = e1 ? xxy.y : __builtin_amdgcn_fmed3f(qxy.y, loxy.y, hixy.y);
+        const float n2 = e2 ? xz : __builtin_amdgcn_fmed3f(qz, hz - R, hz + R);
+        hxy = (f2){n0, n1};
+        hz = n2;
+        t = fetch(n0, n1, n2);
+        if (t >= kSentinel) break;                      // left the grid: sky behind
         cnt.prim_fetch++;
-        dist = t >> 24;
         col = (t >> 16) & 0xff;
         if (col != prev) {
-            if (col == kGlass && !have_glass) {            // glass: blend over the next surface
+            const int ax = e0 ? 0 : (e1 ? 1 : 2);
+            if (col == kGlass && !have_glass) {         // glass: blend over the next surface
                 have_glass = true;
-                gc0 = c0; gc1 = c1; gc2 = c2; gax = ax; gt = te;
+                gxy = hxy; gz = hz; gt = te; gax = ax;
             } else {
-                hit_ax = ax;
+                hit = true;
+                hax = ax;
                 break;
             }
         }
         prev = col;
+        R = (float)(t >> 24);
     }
     if (iter == cap) cnt.cap_hit++;
     // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
     int nrec = 0;
     if (have_glass) {
-        const int st = gax == 0 ? st0 : (gax == 1 ? st1 : st2);
-        const int up = st > 0 ? 0 : 1;
+        const bool pos = gax == 0 ? p0 : (gax == 1 ? p1 : p2);
+        const int up = pos ? 0 : 1;
+        const float r0 = gxy.x - hpxy.x, r1 = gxy.y - hpxy.y, r2 = gz - hpz;   // relative cell
         g0.id = 2;
         g0.color = kGlass;
-        g0.nidx = 2 * gax + (st > 0 ? 1 : 0);
-        g0.c0 = gc0 + cc0 + (gax == 0 ? up : 0);
-        g0.c1 = gc1 + cc1 + (gax == 1 ? up : 0);
-        g0.c2 = gc2 + cc2 + (gax == 2 ? up : 0);
-        g0.f0 = gax == 0 ? 0.0f : (o0 + gt * d0) - (float)gc0;
-        g0.f1 = gax == 1 ? 0.0f : (o1 + gt * d1) - (float)gc1;
-        g0.f2 = gax == 2 ? 0.0f : (o2 + gt * d2) - (float)gc2;
+        g0.nidx = 2 * gax + (pos ? 1 : 0);
+        g0.c0 = (int)r0 + cc0 + (gax == 0 ? up : 0);
+        g0.c1 = (int)r1 + cc1 + (gax == 1 ? up : 0);
+        g0.c2 = (int)r2 + cc2 + (gax == 2 ? up : 0);
+        g0.f0 = gax == 0 ? 0.0f : (o0 + gt * d0) - r0;
+        g0.f1 = gax == 1 ? 0.0f : (o1 + gt * d1) - r1;
+        g0.f2 = gax == 2 ? 0.0f : (o2 + gt * d2) - r2;
         nrec = 1;
     }
-    if (hit_ax >= 0) {
+    if (hit) {
         Surf &h = have_glass ? g1 : g0;
-        const int st = hit_ax == 0 ? st0 : (hit_ax == 1 ? st1 : st2);
-        const int up = st > 0 ? 0 : 1;
+        const bool pos = hax == 0 ? p0 : (hax == 1 ? p1 : p2);
+        const int up = pos ? 0 : 1;
+        const float r0 = hxy.x - hpxy.x, r1 = hxy.y - hpxy.y, r2 = hz - hpz;
         h.id = col == kGlass ? 2 : 0;
         h.color = col;
-        h.nidx = 2 * hit_ax + (st > 0 ? 1 : 0);
-        h.c0 = c0 + cc0 + (hit_ax == 0 ? up : 0);
-        h.c1 = c1 + cc1 + (hit_ax == 1 ? up : 0);
-        h.c2 = c2 + cc2 + (hit_ax == 2 ? up : 0);
-        h.f0 = hit_ax == 0 ? 0.0f : (o0 + te * d0) - (float)c0;
-        h.f1 = hit_ax == 1 ? 0.0f : (o1 + te * d1) - (float)c1;
-        h.f2 = hit_ax == 2 ? 0.0f : (o2 + te * d2) - (float)c2;
+        h.nidx = 2 * hax + (pos ? 1 : 0);
+        h.c0 = (int)r0 + cc0 + (hax == 0 ? up : 0);
+        h.c1 = (int)r1 + cc1 + (hax == 1 ? up : 0);
+        h.c2 = (int)r2 + cc2 + (hax == 2 ? up : 0);
+        h.f0 = hax == 0 ? 0.0f : (o0 + te * d0) - r0;
+        h.f1 = hax == 1 ? 0.0f : (o1 + te * d1) - r1;
+        h.f2 = hax == 2 ? 0.0f : (o2 + te * d2) - r2;
         nrec++;
     }
     return nrec;
@@ -507,6 +535,14 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
     }
 }
 
+// =====================================================================
+// Two pixels per lane (PAIR): each lane steps two independent rays back to
+// back, so the dependent texel-load -> ALU chains of both overlap (ILP 2).
+// The kernel is latency-bound at the 8-waves/SIMD maximum (halving the waves
+// costs 1.46x), so a second independent chain per wave is the lever.
+// Same arithmetic, same results as the one-pixel path.
+// =====================================================================
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     unsigned long long s = v;
 #pragma unroll
@@ -514,6 +550,36 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     return s;
 }
 
+template <int FMT>
+__device__ __forceinline__ void store_pixel(const KernelArgs &a, size_t idx, const float rgba[4]) {
+    if (FMT == VX_PIXEL_RGBA32F) {
+        reinterpret_cast<float4 *>(a.out)[idx] = make_float4(rgba[0], rgba[1], rgba[2], rgba[3]);
+    } else {
+        uint32_t pk = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) pk |= (uint32_t)(gclamp(rgba[i], 0.0f, 1.0f) * 255.0f + 0.5f) << (8 * i);
+        reinterpret_cast<uint32_t *>(a.out)[idx] = pk;
+    }
+}
+
+// view ray of pixel (px, py): nx = (2px+1)/w - 1, ny = 1 - (2py+1)/h with exact quotients
+__device__ __forceinline__ void view_ray(const FrameConsts &F, int px, int py, float &d0, float &d1, float &d2) {
+    const float nx = div_const((float)(2 * px + 1), F.fw, F.rcp_w) - 1.0f;
+    const float ny = 1.0f - div_const((float)(2 * py + 1), F.fh, F.rcp_h);
+    d0 = (F.fwd[0] + nx * F.right[0]) + ny * F.up[0];
+    d1 = (F.fwd[1] + nx * F.right[1]) + ny * F.up[1];
+    d2 = (F.fwd[2] + nx * F.right[2]) + ny * F.up[2];
+}
+
+__device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float rgba[4]) {
+    const int pc = n == 0 ? 0 : g0.color;
+    rgba[0] = pc < 22 ? kPalette[pc][0] : 1.0f;
+    rgba[1] = pc < 22 ? kPalette[pc][1] : 1.0f;
+    rgba[2] = pc < 22 ? kPalette[pc][2] : 1.0f;
+    rgba[3] = 1.0f;
+}
+
+// Lane = pixel, wave = 8x8 tile, workgroup = 16x16 pixels.
 template <int FMT, bool STATS, bool TILED>
 __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
     // unorm8 -> float table: b/255 as IEEE quotients (render.frag:38 decode)
@@ -523,41 +589,32 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lx = ((wave & 1) << 3) | (lane & 7);
     const int ly = ((wave >> 1) << 3) | (lane >> 3);
-    int px, py;
-    size_t out_idx;
+    int ox, oy, tx0 = 0, ty0 = 0, tile_k = 0;
     if (TILED) {
-        const int sub_per_row = a.tile_size >> 4;
-        const int bpt = sub_per_row * sub_per_row;   // 16x16 blocks per tile
-        const int k = blockIdx.x / bpt, sub = blockIdx.x % bpt;
-        const int tid = a.tile_ids[k];
-        const int tx = ((sub % sub_per_row) << 4) + lx, ty = ((sub / sub_per_row) << 4) + ly;
-        px = (tid % a.tiles_x) * a.tile_size + tx;
-        py = (tid / a.tiles_x) * a.tile_size + ty;
-        out_idx = (size_t)k * a.tile_size * a.tile_size + (size_t)ty * a.tile_size + tx;
+        const int bpt = (a.tile_size >> 4) * (a.tile_size >> 4);
+        tile_k = blockIdx.x / bpt;
+        const int sub = blockIdx.x % bpt;
+        const int tid = a.tile_ids[tile_k];
+        tx0 = (sub % (a.tile_size >> 4)) << 4;
+        ty0 = (sub / (a.tile_size >> 4)) << 4;
+        ox = (tid % a.tiles_x) * a.tile_size + tx0;
+        oy = (tid / a.tiles_x) * a.tile_size + ty0;
     } else {
-        px = (blockIdx.x << 4) + lx;
-        py = (blockIdx.y << 4) + ly;
-        out_idx = (size_t)py * a.w + px;
+        ox = blockIdx.x << 4;
+        oy = blockIdx.y << 4;
     }
+    const int px = ox + lx, py = oy + ly;
     const FrameConsts &F = a.fc;
-    const bool active = px < a.w && py < a.h;
     Counters cnt = {0, 0, 0, 0, 0, 0};
-    unsigned n_sky = 0, n_block = 0, n_glass = 0;
-    if (active) {
-        // nx = (2px+1)/w - 1, ny = 1 - (2py+1)/h with exact quotients
-        const float nx = div_const((float)(2 * px + 1), F.fw, F.rcp_w) - 1.0f;
-        const float ny = 1.0f - div_const((float)(2 * py + 1), F.fh, F.rcp_h);
-        const float d0 = (F.fwd[0] + nx * F.right[0]) + ny * F.up[0];
-        const float d1 = (F.fwd[1] + nx * F.right[1]) + ny * F.up[1];
-        const float d2 = (F.fwd[2] + nx * F.right[2]) + ny * F.up[2];
+    unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
+    if (px < a.w && py < a.h) {
+        float d0, d1, d2;
+        view_ray(F, px, py, d0, d1, d2);
         Surf g[2];
         const int n = primary(a, d0, d1, d2, g[0], g[1], cnt);
         float rgba[4];
         if (F.flags & VX_FLAG_PRIMARY_ONLY) {
-            const int pc = n == 0 ? 0 : g[0].color;
-            rgba[0] = pc < 22 ? kPalette[pc][0] : 1.0f;
-            rgba[1] = pc < 22 ? kPalette[pc][1] : 1.0f;
-            rgba[2] = pc < 22 ? kPalette[pc][2] : 1.0f;
+            primary_only_colour(n, g[0], rgba);
             n_sky = n == 0;
             n_glass = n != 0 && g[0].id == 2;
             n_block = n != 0 && g[0].id != 2;
@@ -579,18 +636,15 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
             }
         }
         rgba[3] = 1.0f;
-        if (FMT == VX_PIXEL_RGBA32F) {
-            reinterpret_cast<float4 *>(a.out)[out_idx] = make_float4(rgba[0], rgba[1], rgba[2], rgba[3]);
-        } else {
-            uint32_t pk = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) pk |= (uint32_t)(gclamp(rgba[i], 0.0f, 1.0f) * 255.0f + 0.5f) << (8 * i);
-            reinterpret_cast<uint32_t *>(a.out)[out_idx] = pk;
-        }
+        const size_t idx = TILED ? (size_t)tile_k * a.tile_size * a.tile_size + (size_t)(ty0 + ly) * a.tile_size +
+                                       (tx0 + lx)
+                                 : (size_t)py * a.w + px;
+        store_pixel<FMT>(a, idx, rgba);
+        n_px = 1;
     }
     if (STATS) {
         unsigned long long v[ST_COUNT];
-        v[ST_PIXELS] = wave_sum(active ? 1u : 0u);
+        v[ST_PIXELS] = wave_sum(n_px);
         v[ST_SKY] = wave_sum(n_sky);
         v[ST_BLOCK] = wave_sum(n_block);
         v[ST_GLASS] = wave_sum(n_glass);
@@ -621,7 +675,8 @@ __global__ void k_detile(const T *tiles, T *frame, int w, int h, int ts, int til
     if (x < w && y < h) frame[(size_t)y * w + x] = tiles[i];
 }
 
-// ---- A channel: capped Chebyshev distance to the nearest non-air cell ----
+// ---- A channel: half-size R = D - 1 of the air box around a cell, D the capped
+// Chebyshev distance to the nearest non-air cell (0 for non-air cells) ----
 __global__ void k_dist_x(const uint32_t *field, uint8_t *g1, int X, int Y, int Z, int cap) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t N = (size_t)X * Y * Z;
@@ -657,7 +712,7 @@ __global__ void k_dist_yz(const uint8_t *gin, uint8_t *gout, uint32_t *field, in
         best = m < best ? m : best;
     }
     if (axis == 1) gout[i] = (uint8_t)best;
-    else field[i] = (field[i] & 0x00ffffffu) | ((uint32_t)best << 24);
+    else field[i] = (field[i] & 0x00ffffffu) | ((uint32_t)(best > 0 ? best - 1 : 0) << 24);   // A = R
 }
 
 __global__ void k_reduce_stats(unsigned long long *stats) {
@@ -673,21 +728,16 @@ __global__ void k_reduce_stats(unsigned long long *stats) {
 
 int launch_render(const KernelArgs &a, int fmt, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    dim3 block(256);
-    dim3 grid;
     const bool tiled = a.tile_ids != nullptr;
-    if (tiled) grid = dim3(a.n_tiles * (a.tile_size >> 4) * (a.tile_size >> 4));
-    else grid = dim3((a.w + 15) / 16, (a.h + 15) / 16);
     const bool st = a.stats != nullptr;
-#define VX_LAUNCH(F, S, T) hipLaunchKernelGGL((k_render<F, S, T>), grid, block, 0, s, a)
-    if (fmt == VX_PIXEL_RGBA32F) {
-        if (tiled) { if (st) VX_LAUNCH(0, true, true); else VX_LAUNCH(0, false, true); }
-        else { if (st) VX_LAUNCH(0, true, false); else VX_LAUNCH(0, false, false); }
-    } else {
-        if (tiled) { if (st) VX_LAUNCH(1, true, true); else VX_LAUNCH(1, false, true); }
-        else { if (st) VX_LAUNCH(1, true, false); else VX_LAUNCH(1, false, false); }
-    }
-#undef VX_LAUNCH
+    dim3 block(256);
+    dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_size >> 4) * (a.tile_size >> 4)) : dim3((a.w + 15) / 16, (a.h + 15) / 16);
+#define VX_L(F, S, T) hipLaunchKernelGGL((k_render<F, S, T>), grid, block, 0, s, a)
+#define VX_LT(F, S) do { if (tiled) VX_L(F, S, true); else VX_L(F, S, false); } while (0)
+    if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_LT(0, true); else VX_LT(0, false); }
+    else { if (st) VX_LT(1, true); else VX_LT(1, false); }
+#undef VX_LT
+#undef VX_L
     if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
     return (int)hipGetLastError();
 }
@@ -703,6 +753,37 @@ int launch_detile(const void *tiles, void *frame, int w, int h, int ts, int tile
     else
         hipLaunchKernelGGL(k_detile<uint32_t>, grid, dim3(256), 0, s, (const uint32_t *)tiles, (uint32_t *)frame, w,
                            h, ts, tiles_x, ids, n_tiles);
+    return (int)hipGetLastError();
+}
+
+namespace {
+// linear x-fastest grid <-> the padded field (border cells keep the sentinel)
+__global__ void k_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, int P, int to_padded) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)X * Y * Z) return;
+    const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+    const size_t Xp = (size_t)X + 2 * P, Yp = (size_t)Y + 2 * P;
+    const size_t j = (size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P));
+    if (to_padded) dst[j] = src[i];
+    else dst[i] = src[j];
+}
+}  // namespace
+
+FieldLayout field_layout(int X, int Y, int Z, int cap) {
+    FieldLayout L;
+    L.pad = cap;
+    L.Xp = X + 2 * cap;
+    L.Yp = Y + 2 * cap;
+    L.Zp = Z + 2 * cap;
+    L.texels = (size_t)L.Xp * L.Yp * L.Zp;
+    L.k0 = (size_t)cap * (1 + (size_t)L.Xp + (size_t)L.Xp * L.Yp);
+    return L;
+}
+
+int launch_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, int pad, int to_padded, void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    hipLaunchKernelGGL(k_field_pad, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, src, dst, X,
+                       Y, Z, pad, to_padded);
     return (int)hipGetLastError();
 }
 
