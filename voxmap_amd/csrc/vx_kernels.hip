@@ -277,13 +277,16 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
     cnt.prim_fetch++;
     int prev = (t >> 16) & 0xff;
     float R = (float)(t >> 24);
-    bool have_glass = false, hit = false;
+    // ints, not bools: loop-carried and live-out lane masks cost SALU merges per step
+    int have_glass = 0, stop;
     f2 gxy = {0.0f, 0.0f};
-    float gz = 0.0f, gt = 0.0f, te = 0.0f;
-    int gax = 0, hax = 0, col = 0;
+    float gz = 0.0f, gt = 0.0f, te;
+    int gax = 0, hax, col;
+    // One exit test per step (a sentinel texel, or a colour change that is not
+    // the first glass entry); the step counter is wave-uniform.
     const int cap = 4 * (a.X + a.Y + a.Z);
-    int iter = 0;
-    for (; iter < cap; iter++) {
+    int it = 0;
+    do {
         const f2 Rv = {R, R};
         const f2 Axy = __builtin_elementwise_fma(sxy, Rv, hxy);
         const float Az = __builtin_fmaf(sz, R, hz);
@@ -307,25 +310,26 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
         const float n2 = e2 ? xz : __builtin_amdgcn_fmed3f(qz, hz - R, hz + R);
         hxy = (f2){n0, n1};
         hz = n2;
+        hax = e0 ? 0 : (e1 ? 1 : 2);
+        asm volatile("" : "+v"(hax));                  // keep e0/e1 from living past the loop
         t = fetch(n0, n1, n2);
-        if (t >= kSentinel) break;                      // left the grid: sky behind
-        cnt.prim_fetch++;
+        const bool oob = t >= kSentinel;               // left the grid: sky behind
+        cnt.prim_fetch += oob ? 0u : 1u;
         col = (t >> 16) & 0xff;
-        if (col != prev) {
-            const int ax = e0 ? 0 : (e1 ? 1 : 2);
-            if (col == kGlass && !have_glass) {         // glass: blend over the next surface
-                have_glass = true;
-                gxy = hxy; gz = hz; gt = te; gax = ax;
-            } else {
-                hit = true;
-                hax = ax;
-                break;
-            }
+        const bool change = col != prev && !oob;
+        const bool gfirst = change && col == kGlass && have_glass == 0;
+        if (gfirst) {                                  // glass: blend over the next surface
+            have_glass = 1;
+            gxy = hxy; gz = hz; gt = te; gax = hax;
         }
+        stop = (oob || (change && !gfirst)) ? 1 : 0;
+        asm volatile("" : "+v"(stop));
         prev = col;
         R = (float)(t >> 24);
-    }
-    if (iter == cap) cnt.cap_hit++;
+    } while (stop == 0 && ++it < cap);
+    asm volatile("" : "+v"(col));
+    if (stop == 0) cnt.cap_hit++;
+    const bool hit = stop != 0 && t < kSentinel;
     // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
     int nrec = 0;
     if (have_glass) {
