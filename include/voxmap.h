@@ -108,8 +108,12 @@ typedef struct vx_stats {
 /* --- scene lifetime ------------------------------------------------------ */
 int vx_scene_create(const vx_scene_desc *desc, vx_scene **out);
 void vx_scene_destroy(vx_scene *scene);
-/* Copy the device-resident field (RGBA8, A = primary-march distance) back. */
+/* Copy the device-resident field back (RGBA8 X*Y*Z, x fastest).  The device
+ * keeps one copy per ray octant (bit 0/1/2: x/y/z direction negative) whose A
+ * byte is that octant's air-cube size for the primary traversal (DESIGN.md
+ * §3); R, G, B are map.bin's.  vx_scene_read_field reads octant 0. */
 int vx_scene_read_field(vx_scene *scene, void *host_out, size_t cap);
+int vx_scene_read_field_copy(vx_scene *scene, int octant, void *host_out, size_t cap);
 int vx_scene_dims(const vx_scene *scene, int dims[3]);
 
 /* --- rendering (replaces gl.drawArrays at render.js:297 + the shaders) --- */

@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(_HERE, "build", "libvxo.so")
 
 class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
-                ("noise_w", C.c_int), ("noise_h", C.c_int)]
+                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_r", C.c_void_p * 8)]
 
 
 class OStats(C.Structure):
@@ -72,7 +72,7 @@ def lib():
         L.vxo_exp2.argtypes = [C.c_float]
         L.vxo_exp2.restype = C.c_float
         L.vxo_field_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
-        L.vxo_field_dist.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.vxo_field_octant.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         _lib = L
     return _lib
 
@@ -80,12 +80,15 @@ def lib():
 class Oracle:
     """Scalar restatement of render.frag over one field + noise texture."""
 
-    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray):
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32):
         self.field = np.ascontiguousarray(field_zyx4, np.uint8)
         self.noise = np.ascontiguousarray(noise_hw4, np.uint8)
         Z, Y, X, _ = self.field.shape
         H, W, _ = self.noise.shape
-        self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H)
+        # the primary traversal's octant cubes (vxo_field_octant), from the colours
+        self.oct_r = [field_octant(self.field, o, cap) for o in range(8)]
+        self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
+                         (C.c_void_p * 8)(*[r.ctypes.data for r in self.oct_r]))
 
     def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
         """RGBA fp32 (h, w, 4); rows not in (row0::row_step) are NaN."""
@@ -129,10 +132,12 @@ def field_build(color_zyx: np.ndarray) -> np.ndarray:
     return out
 
 
-def field_dist(field_zyx4: np.ndarray, cap: int = 32) -> np.ndarray:
-    out = np.ascontiguousarray(field_zyx4, np.uint8).copy()
-    Z, Y, X, _ = out.shape
-    lib().vxo_field_dist(out.ctypes.data, X, Y, Z, cap)
+def field_octant(field_zyx4: np.ndarray, oct: int, cap: int = 32) -> np.ndarray:
+    """(Z, Y, X) uint8: size of the all-air cube ahead of each cell for ray octant ``oct``."""
+    f = np.ascontiguousarray(field_zyx4, np.uint8)
+    Z, Y, X, _ = f.shape
+    out = np.empty((Z, Y, X), np.uint8)
+    lib().vxo_field_octant(f.ctypes.data, X, Y, Z, cap, oct, out.ctypes.data)
     return out
 
 

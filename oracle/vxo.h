@@ -36,6 +36,7 @@ typedef struct {
     const uint8_t *field;     /* RGBA8 X*Y*Z texels, x fastest (render.js:62) */
     const uint8_t *noise;     /* RGBA8 noise texture (render.js:138-149) */
     int noise_w, noise_h;
+    const uint8_t *oct_r[8];  /* vxo_field_octant per ray octant (primary traversal) */
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */
@@ -110,9 +111,10 @@ float vxo_exp2(float x);
 /* Build the RGBA8 field from a palette-index grid (x fastest), restating
  * sdf.cpp:405-470 literally (serial x->y->z order, clamped-index quirks). */
 void vxo_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba);
-/* Fill the A channel with the capped Chebyshev distance used by the primary
- * march (A is written 0 by sdf.cpp:469 and unused by the GLSL). */
-void vxo_field_dist(uint8_t *rgba, int X, int Y, int Z, int cap);
+/* Per-cell size r of the all-air cube ahead of the cell for ray octant oct
+ * (bit 0/1/2: x/y/z direction negative), capped: the primary traversal's own
+ * data, X*Y*Z bytes into r_out. */
+void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, uint8_t *r_out);
 
 #ifdef __cplusplus
 }

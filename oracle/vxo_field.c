@@ -17,10 +17,10 @@
  * The reference C++ itself is NOT compiled (SURVEY.md §8c permission denial);
  * this is a from-text restatement.
  *
- * vxo_field_dist: the build's own A-channel contents: the
- * half-size R of the all-air box around each cell, R = D - 1 for the capped
- * Chebyshev distance D >= 1 to the nearest non-air cell, 0 for non-air cells
- * (so A <= cap - 1 <= 254; 255 is free for the kernels' out-of-grid sentinel).
+ * vxo_field_octant: the build's own primary-traversal data:
+ * per octant of ray directions, the size r of the all-air cube ahead of each
+ * cell (r <= cap - 1 <= 254; the kernels keep 255 for their out-of-grid
+ * sentinel).
  */
 #include "vxo.h"
 #include <stdlib.h>
@@ -102,57 +102,57 @@ void vxo_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba) {
     free(c.sdf);
 }
 
-/* Capped Chebyshev distance to the nearest non-air cell (B != 0), separable:
- * D = min_z' max(|dz|, min_y' max(|dy|, min_x' |dx|)). */
-void vxo_field_dist(uint8_t *rgba, int X, int Y, int Z, int cap) {
-    size_t N = (size_t)X * Y * Z;
+/* Octant box half-size: for octant o (bit 0: x negative,
+ * bit 1: y, bit 2: z; a zero direction component counts as positive) the
+ * largest L <= cap such that the cube of side L with corner c extending toward
+ * the octant holds no non-air cell (B != 0) of the grid; r = L - 1 (0 for
+ * non-air cells).  L = min over forward non-air q of max_i (q_i - c_i) s_i,
+ * separable: L = min_dz max(dz, min_dy max(dy, min_dx dx)) over dx, dy, dz in
+ * [0, cap).  Cells outside the grid count as air. */
+void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, uint8_t *r_out) {
+    const size_t N = (size_t)X * Y * Z;
+    const int sx = oct & 1 ? -1 : 1, sy = oct & 2 ? -1 : 1, sz = oct & 4 ? -1 : 1;
     unsigned char *g1 = (unsigned char *)malloc(N), *g2 = (unsigned char *)malloc(N);
-    const int dims[3] = {X, Y, Z};
-    (void)dims;
-    /* pass x: 1-D distance along x */
-    for (int z = 0; z < Z; z++)
+#define I3(x, y, z) ((size_t)(x) + (size_t)X * ((size_t)(y) + (size_t)Y * (size_t)(z)))
+#pragma omp parallel for schedule(static)
+    for (int z = 0; z < Z; z++)          /* pass x: forward run to the first non-air cell */
         for (int y = 0; y < Y; y++)
             for (int x = 0; x < X; x++) {
                 int best = cap;
-                for (int k = 0; k < cap && best > k; k++) {
-                    int xa = x - k, xb = x + k;
-                    if ((xa >= 0 && rgba[4 * ((size_t)xa + (size_t)X * ((size_t)y + (size_t)Y * z)) + 2]) ||
-                        (xb < X && rgba[4 * ((size_t)xb + (size_t)X * ((size_t)y + (size_t)Y * z)) + 2]))
-                        best = k;
+                for (int k = 0; k < cap; k++) {
+                    const int xx = x + k * sx;
+                    if (xx < 0 || xx >= X) break;
+                    if (rgba[4 * I3(xx, y, z) + 2]) { best = k; break; }
                 }
-                g1[(size_t)x + (size_t)X * ((size_t)y + (size_t)Y * z)] = (unsigned char)best;
+                g1[I3(x, y, z)] = (unsigned char)best;
             }
-    /* pass y */
-    for (int z = 0; z < Z; z++)
+#pragma omp parallel for schedule(static)
+    for (int z = 0; z < Z; z++)          /* pass y */
         for (int y = 0; y < Y; y++)
             for (int x = 0; x < X; x++) {
                 int best = cap;
-                for (int k = -(cap - 1); k <= cap - 1; k++) {
-                    int yy = y + k;
-                    if (yy < 0 || yy >= Y) continue;
-                    int v = g1[(size_t)x + (size_t)X * ((size_t)yy + (size_t)Y * z)];
-                    int ak = k < 0 ? -k : k;
-                    int m = v > ak ? v : ak;
+                for (int k = 0; k < cap; k++) {
+                    const int yy = y + k * sy;
+                    if (yy < 0 || yy >= Y) break;
+                    const int v = g1[I3(x, yy, z)], m = v > k ? v : k;
                     if (m < best) best = m;
                 }
-                g2[(size_t)x + (size_t)X * ((size_t)y + (size_t)Y * z)] = (unsigned char)best;
+                g2[I3(x, y, z)] = (unsigned char)best;
             }
-    /* pass z -> A channel */
-    for (int z = 0; z < Z; z++)
+#pragma omp parallel for schedule(static)
+    for (int z = 0; z < Z; z++)          /* pass z -> r */
         for (int y = 0; y < Y; y++)
             for (int x = 0; x < X; x++) {
                 int best = cap;
-                for (int k = -(cap - 1); k <= cap - 1; k++) {
-                    int zz = z + k;
-                    if (zz < 0 || zz >= Z) continue;
-                    int v = g2[(size_t)x + (size_t)X * ((size_t)y + (size_t)Y * zz)];
-                    int ak = k < 0 ? -k : k;
-                    int m = v > ak ? v : ak;
+                for (int k = 0; k < cap; k++) {
+                    const int zz = z + k * sz;
+                    if (zz < 0 || zz >= Z) break;
+                    const int v = g2[I3(x, y, zz)], m = v > k ? v : k;
                     if (m < best) best = m;
                 }
-                rgba[4 * ((size_t)x + (size_t)X * ((size_t)y + (size_t)Y * z)) + 3] =
-                    (unsigned char)(best > 0 ? best - 1 : 0);
+                r_out[I3(x, y, z)] = (unsigned char)(best > 0 ? best - 1 : 0);
             }
+#undef I3
     free(g1);
     free(g2);
 }

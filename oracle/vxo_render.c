@@ -234,13 +234,14 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
  * last and blended (render.js:84-86); the surface behind a glass entry is the
  * next colour change, which is never glass, so one blend layer is exact.
  *
- * Traversal ("box-exit" stepping): from the current cell c with A-channel
- * box half-size R (vxo_field_dist) every cell of the box c +- R is air, so the ray
- * jumps straight to the face where it leaves that box: per axis the crossing
- * time of the box's far face, the earliest one (ties x, then y, then z) is the
- * exit axis; the next cell is one past the box on that axis and floor() of the
- * exit point, clamped into the box, on the others.  With R = 0 (next to or
- * inside a non-air cell) the box is the cell itself and the step is an exact DDA step.
+ * Traversal ("box-exit" stepping): from the current cell c, the ray's octant
+ * (direction signs s, zero counted positive) has the all-air cube
+ * B = [c, c + R*s] ahead of c (R = vxo_field_octant), so the ray jumps straight
+ * to the face where it leaves B: per axis the crossing time of the far face
+ * (c + R + 1 for s > 0, c - R for s < 0), the earliest one (ties x, then y,
+ * then z) is the exit axis; the next cell is one past B on that axis and
+ * floor() of the exit point, clamped into B, on the others.  With R = 0 (next
+ * to or inside a non-air cell) B is the cell itself: an exact DDA step.
  * Camera-relative cells keep the fp32 coordinates small.
  */
 static inline int in_grid(const vxo_scene *s, const int a[3]) {
@@ -284,8 +285,11 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
     int abs_c[3] = {c[0] + cc[0], c[1] + cc[1], c[2] + cc[2]};
     const uint8_t *tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
     (*fetches)++;
+    const int oct = (d[0] < 0.0f ? 1 : 0) | (d[1] < 0.0f ? 2 : 0) | (d[2] < 0.0f ? 4 : 0);
+    const uint8_t *octr = s->oct_r[oct];
+#define OCT_R(a) ((int)octr[(size_t)(a)[0] + (size_t)s->X * ((size_t)(a)[1] + (size_t)s->Y * (size_t)(a)[2])])
     int prev = tx[2];
-    int R = tx[3];
+    int R = OCT_R(abs_c);
     int nrec = 0;
     const int cap = 4 * (dims[0] + dims[1] + dims[2]);
     for (int iter = 0; iter < cap; iter++) {
@@ -298,8 +302,9 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
             if (i == a) {
                 c[i] = c[i] + stp[i] * (R + 1);
             } else {
-                int v = g_f2i(floorf(o[i] + te * d[i]));
-                c[i] = v < c[i] - R ? c[i] - R : (v > c[i] + R ? c[i] + R : v);
+                const int v = g_f2i(floorf(o[i] + te * d[i]));
+                const int lo = d[i] < 0.0f ? c[i] - R : c[i], hi = d[i] < 0.0f ? c[i] : c[i] + R;
+                c[i] = v < lo ? lo : (v > hi ? hi : v);
             }
         }
         abs_c[0] = c[0] + cc[0]; abs_c[1] = c[1] + cc[1]; abs_c[2] = c[2] + cc[2];
@@ -307,7 +312,7 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
         tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
         (*fetches)++;
         const int col = tx[2];
-        R = tx[3];                                 /* air box half-size */
+        R = OCT_R(abs_c);                          /* air cube ahead */
         if (col != prev) {
             vxo_gbuf *h = &g[nrec];
             h->color = col;
@@ -330,6 +335,7 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
     }
     *cap_hit = 1;
     return nrec;
+#undef OCT_R
 }
 
 void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3]) {

@@ -30,7 +30,7 @@ W, H = 64, 48
 
 def inputs(case):
     g = scenes.small_proc(case["seed"], dims=tuple(case["dims"]), n_boxes=16, n_glass=case.get("n_glass", 6))
-    field = oracle.field_dist(vx.field_build(g), 32)
+    field = vx.field_build(g)
     noise = vx.noise_synth(0)
     fr = vx.make_frame(tuple(case["sbj"]), tuple(case["rot"]), W, H)
     return field, noise, fr

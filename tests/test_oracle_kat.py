@@ -141,7 +141,7 @@ def test_empty_map_every_sun_facing_fragment_lit(O):
     import voxmap_amd as vx
     g = np.zeros((16, 96, 128), np.uint8)
     g[0] = 2
-    field = O.field_dist(_field(g), 32)
+    field = _field(g)
     noise = np.full((8, 8, 4), 128, np.uint8)
     o = O.Oracle(field, noise)
     fr = vx.make_frame((64.0, 48.0, 10.0), (1e-4, 0.0, -0.002), 64, 48)
@@ -201,7 +201,7 @@ def test_primary_hits_top_face_analytically(O):
     import voxmap_amd as vx
     from voxmap_amd import scenes
     g = scenes.single_block(dims=(64, 32, 16), at=(20, 12, 1), color=5)
-    field = O.field_dist(_field(g), 32)
+    field = _field(g)
     o = O.Oracle(field, np.zeros((4, 4, 4), np.uint8))
     fr = vx.make_frame((20.4, 12.7, 4.0), (0.08, 0.0, 0.2), 48, 48)
     p = fr.params
@@ -235,7 +235,7 @@ def test_primary_glass_then_behind_and_boundary_rule(O):
     g[1:4, 8, 10:20] = 21          # a glass pane (y = 8)
     g[1:4, 12, 10:20] = 7          # a wall behind it (y = 12)
     g[1:6, 0:16, 31] = 9           # a wall on the grid's x = 31 edge
-    field = O.field_dist(_field(g), 32)
+    field = _field(g)
     o = O.Oracle(field, np.zeros((4, 4, 4), np.uint8))
     fr = vx.make_frame((15.0, 4.0, 2.0), (math.pi / 2, 0.0, 0.0), 16, 16)   # looking +y, level
     d = np.array([0.0, 1.0, 0.01])
@@ -250,20 +250,32 @@ def test_primary_glass_then_behind_and_boundary_rule(O):
     assert n2 == 1 and gb2[0].color == 0 and gb2[0].normal_idx == 0 and gb2[0].cell[0] == 31
 
 
-def test_field_dist_is_air_box_half_size(O):
-    """A channel = R with the box c +- R all air and R + 1 <= cap: brute force
-    Chebyshev distance D to the nearest non-air cell (grid-bounded), R = D - 1."""
+def test_field_octant_is_air_cube_ahead(O):
+    """Octant cube size r: the cube [c, c + r*s] (s = the octant's direction signs)
+    holds no non-air cell, r + 1 <= cap, and r is maximal: brute force over every
+    cell and octant on a small random grid (cells outside the grid count as air)."""
     rng = np.random.default_rng(3)
-    Z, Y, X, cap = 9, 11, 13, 4
-    col = np.where(rng.random((Z, Y, X)) < 0.04, 7, 0).astype(np.uint8)
+    Z, Y, X, cap = 7, 9, 11, 5
+    col = np.where(rng.random((Z, Y, X)) < 0.05, 7, 0).astype(np.uint8)
     field = np.zeros((Z, Y, X, 4), np.uint8)
     field[..., 2] = col
-    got = O.field_dist(field, cap)
-    assert np.array_equal(got[..., :3], field[..., :3])
-    solid = np.argwhere(col != 0)
-    zz, yy, xx = np.meshgrid(np.arange(Z), np.arange(Y), np.arange(X), indexing="ij")
-    D = np.full((Z, Y, X), cap)
-    for z, y, x in solid:
-        D = np.minimum(D, np.maximum(np.maximum(abs(zz - z), abs(yy - y)), abs(xx - x)))
-    assert np.array_equal(got[..., 3], np.maximum(D - 1, 0).astype(np.uint8))
-    assert got[..., 3].max() <= cap - 1           # 255 stays free for the out-of-grid sentinel
+    solid = col != 0
+    for oct in range(8):
+        s = [-1 if oct & b else 1 for b in (1, 2, 4)]        # x, y, z signs
+        got = O.field_octant(field, oct, cap)
+        for z in range(Z):
+            for y in range(Y):
+                for x in range(X):
+                    L = 0
+                    while L < cap:                           # grow the cube while it stays air
+                        xs = [x + s[0] * k for k in range(L + 1)]
+                        ys = [y + s[1] * k for k in range(L + 1)]
+                        zs = [z + s[2] * k for k in range(L + 1)]
+                        xs = [v for v in xs if 0 <= v < X]
+                        ys = [v for v in ys if 0 <= v < Y]
+                        zs = [v for v in zs if 0 <= v < Z]
+                        if solid[np.ix_(zs, ys, xs)].any():
+                            break
+                        L += 1
+                    assert got[z, y, x] == max(L - 1, 0), (oct, x, y, z, got[z, y, x], L)
+        assert got.max() <= cap - 1                   # 255 stays free for the out-of-grid sentinel

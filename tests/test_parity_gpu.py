@@ -76,16 +76,17 @@ def test_small_frames_bit_exact(seed, dims, sbj, rot, noise):
     assert st.primary_cap_hits == 0
 
 
-def test_field_distance_channel_matches_oracle(noise):
+@pytest.mark.parametrize("octant", range(8))
+def test_field_octant_copies_match_oracle(noise, octant):
     import oracle
     import voxmap_amd as vx
-    from voxmap_amd import presets
-    grid = presets.scene_grid("s_proc")
-    field = vx.field_build(grid)
-    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
-        dev = sc.read_field()
+    from voxmap_amd import scenes
+    dims = (160, 72, 20)
+    field = vx.field_build(scenes.small_proc(17, dims=dims, n_boxes=24, n_glass=4))
+    with _scene(vx, field, noise, dims) as sc:
+        dev = sc.read_field(octant)
     assert np.array_equal(dev[..., :3], field[..., :3])
-    assert np.array_equal(dev, oracle.field_dist(field, 32))
+    assert np.array_equal(dev[..., 3], oracle.field_octant(field, octant, 32))
 
 
 @pytest.fixture(scope="module")

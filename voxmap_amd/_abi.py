@@ -69,6 +69,7 @@ SIGNATURES = [
     ("vx_scene_create", C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_void_p)]),
     ("vx_scene_destroy", None, [C.c_void_p]),
     ("vx_scene_read_field", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("vx_scene_read_field_copy", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("vx_scene_dims", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     ("vx_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
                             C.c_void_p, C.c_int, C.c_void_p, C.POINTER(Stats)]),

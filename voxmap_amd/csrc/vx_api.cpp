@@ -148,25 +148,28 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         if (gb) (void)hipFree(gb);
         return fail(set_error(VX_EDEVICE, std::string("scene upload failed: ") + hipGetErrorString(e)));
     }
-    // A channel: primary-march distance, computed in HBM
-    int lrc = launch_field_dist(s->d_field, X, Y, Z, cap, ga, gb, s->stream);
-    e = hipStreamSynchronize(s->stream);
+    // 8 octant copies in the padded layout: each copy's A
+    // channel is computed in place in the linear upload, then scattered into
+    // the copy, whose border keeps the out-of-grid sentinel
+    uint32_t *copies = nullptr;
+    int lrc = 0;
+    if ((e = hipMalloc(&copies, 8 * L.texels * 4)) == hipSuccess &&
+        (e = hipMemsetD32Async((hipDeviceptr_t)copies, 0xFF000000u, 8 * L.texels, s->stream)) == hipSuccess) {
+        for (int oct = 0; oct < 8 && !lrc; oct++) {
+            lrc = launch_field_octant(s->d_field, X, Y, Z, cap, oct, ga, gb, s->stream);
+            if (!lrc) lrc = launch_field_pad(s->d_field, copies + oct * L.texels, X, Y, Z, L.pad, 1, s->stream);
+        }
+        e = hipStreamSynchronize(s->stream);
+    }
     (void)hipFree(ga);
     (void)hipFree(gb);
-    if (lrc != 0 || e != hipSuccess)
-        return fail(set_error(VX_EDEVICE, std::string("field distance pass failed: ") +
+    if (lrc != 0 || e != hipSuccess) {
+        if (copies) (void)hipFree(copies);
+        return fail(set_error(VX_EDEVICE, std::string("field preparation failed: ") +
                                               hipGetErrorString(lrc ? (hipError_t)lrc : e)));
-    // into the padded layout the kernels read (border = out-of-grid sentinel)
-    uint32_t *padded = nullptr;
-    if ((e = hipMalloc(&padded, L.texels * 4)) != hipSuccess ||
-        (e = hipMemsetD32Async((hipDeviceptr_t)padded, 0xFF000000u, L.texels, s->stream)) != hipSuccess ||
-        (e = (hipError_t)launch_field_pad(s->d_field, padded, X, Y, Z, L.pad, 1, s->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
-        if (padded) (void)hipFree(padded);
-        return fail(set_error(VX_EDEVICE, std::string("field padding failed: ") + hipGetErrorString(e)));
     }
     (void)hipFree(s->d_field);
-    s->d_field = padded;
+    s->d_field = copies;
     s->L = L;
     *out = s;
     return VX_OK;
@@ -193,14 +196,18 @@ int vx_scene_dims(const vx_scene *s, int dims[3]) {
     return VX_OK;
 }
 
-int vx_scene_read_field(vx_scene *s, void *host_out, size_t cap) {
+int vx_scene_read_field(vx_scene *s, void *host_out, size_t cap) { return vx_scene_read_field_copy(s, 0, host_out, cap); }
+
+int vx_scene_read_field_copy(vx_scene *s, int octant, void *host_out, size_t cap) {
     if (!s || !host_out) return set_error(VX_EINVAL, "vx_scene_read_field: null argument");
+    if (octant < 0 || octant > 7) return set_error(VX_EINVAL, "vx_scene_read_field_copy: octant must be 0..7");
     const size_t n = (size_t)s->X * s->Y * s->Z * 4;
     if (cap < n) return set_error(VX_EINVAL, "vx_scene_read_field: buffer too small");
     VX_HIP(hipSetDevice(s->device));
     uint32_t *lin = nullptr;
     VX_HIP(hipMalloc(&lin, n));
-    hipError_t e = (hipError_t)launch_field_pad(s->d_field, lin, s->X, s->Y, s->Z, s->L.pad, 0, s->stream);
+    hipError_t e = (hipError_t)launch_field_pad(s->d_field + (size_t)octant * s->L.texels, lin, s->X, s->Y, s->Z,
+                                                 s->L.pad, 0, s->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, lin, n, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(lin);
@@ -266,7 +273,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.Xp = s->L.Xp;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
     a.k0 = (unsigned)s->L.k0;
-    a.texels = (unsigned)s->L.texels;
+    a.copy_texels = (unsigned)s->L.texels;
     a.kcam = (unsigned)(p->cam_cell[0] + s->L.pad) + (unsigned)a.Xp * (unsigned)(p->cam_cell[1] + s->L.pad) +
              a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);   // mod 2^32
 

@@ -37,7 +37,7 @@ struct FrameConsts {
 
 // Parameters of one render launch (passed by value to the kernel).
 struct KernelArgs {
-    const uint32_t *field;   // RGBA8 texels, x fastest (render.js:62), padded (FieldLayout)
+    const uint32_t *field;   // 8 octant copies of the padded field (FieldLayout)
     const uint32_t *noise;   // RGBA8 noise texels
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
@@ -53,7 +53,7 @@ struct KernelArgs {
     int Xp;                  // padded row length (FieldLayout)
     unsigned XpYp;           // padded slice size
     unsigned k0;             // padded index of grid cell (0, 0, 0)
-    unsigned texels;         // padded texel count
+    unsigned copy_texels;    // texels per octant copy (FieldLayout::texels)
     unsigned kcam;           // padded index of the camera cell, mod 2^32
     FrameConsts fc;
 };
@@ -65,11 +65,12 @@ enum StatSlot {
     ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_COUNT
 };
 
-// Field layout in HBM: the X x Y x Z grid (x fastest, as map.bin) inside a
-// border of pad = cap sentinel texels on every side.
+// Field layout in HBM: 8 copies, one per ray octant, each the
+// X x Y x Z grid (x fastest, as map.bin; A = the octant's air-cube size)
+// inside a border of pad = cap sentinel texels on every side.
 struct FieldLayout {
     int pad, Xp, Yp, Zp;
-    size_t texels;           // Xp * Yp * Zp
+    size_t texels;           // Xp * Yp * Zp, one copy
     size_t k0;               // index of grid cell (0, 0, 0)
 };
 FieldLayout field_layout(int X, int Y, int Z, int cap);
@@ -80,7 +81,8 @@ int launch_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, in
 int launch_render(const KernelArgs &a, int pixel_format, void *stream);
 int launch_detile(const void *tiles, void *frame, int w, int h, int tile_size, int tiles_x,
                   const int *tile_ids, int n_tiles, int pixel_format, void *stream);
-int launch_field_dist(uint32_t *field, int X, int Y, int Z, int cap, uint8_t *scratch_a,
-                      uint8_t *scratch_b, void *stream);
+// A channel of octant copy `oct` (in place in a linear grid upload)
+int launch_field_octant(uint32_t *field, int X, int Y, int Z, int cap, int oct, uint8_t *scratch_a,
+                        uint8_t *scratch_b, void *stream);
 
 }  // namespace vx

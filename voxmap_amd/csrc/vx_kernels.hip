@@ -107,25 +107,20 @@ struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
 };
 
-// Field in HBM: the reference's x-fastest texels inside a border of P = cap
-// sentinel cells (A = 255, never a real value: A <= cap - 1 <= 254), so the
-// primary traversal detects leaving the grid from the texel it loads.  Texels
-// go through buffer resources: 32-bit byte offsets (fields are < 2 GiB) and
-// hardware range checking (out-of-range reads return 0).
+// Field in HBM: 8 copies, one per octant of ray directions, each the
+// reference's x-fastest texels (R, G, B as map.bin) with A = the octant's
+// air-cube size, inside a border of P = cap sentinel cells (A = 255, never a
+// real value: A <= cap - 1 <= 254), so the primary traversal detects leaving
+// the grid from the texel it loads.  A pixel reads only its primary ray's
+// copy.  Every read is in bounds: the traversal stays within P of the grid,
+// march() returns before reading outside it, the AO sample clamps.
 constexpr uint32_t kSentinel = 0xFF000000u;
 
-// grid-origin based: texel (x, y, z) of the unpadded grid at x + Xp*y + XpYp*z
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t field_rsrc(const KernelArgs &a) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)(a.field + a.k0), 0, (int)((a.texels - a.k0) * 4u), 0x00020000);
-}
-// buffer-start based (primary traversal: padded indices)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t field_rsrc_padded(const KernelArgs &a) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)a.field, 0, (int)(a.texels * 4u), 0x00020000);
-}
-// Xp < 2^16 and XpYp < 2^23 (vx_scene_create), so full-rate 24-bit multiplies.
-__device__ __forceinline__ uint32_t texel(const KernelArgs &a, int x, int y, int z) {
+// fb = the pixel's copy at grid cell (0, 0, 0); Xp < 2^16 and XpYp < 2^23
+// (vx_scene_create), so full-rate 24-bit multiplies.
+__device__ __forceinline__ uint32_t texel(const uint32_t *fb, const KernelArgs &a, int x, int y, int z) {
     const unsigned idx = (unsigned)x + __umul24((unsigned)a.Xp, (unsigned)y) + __umul24(a.XpYp, (unsigned)z);
-    return __builtin_amdgcn_raw_buffer_load_b32(field_rsrc(a), idx * 4u, 0, 0);
+    return fb[idx];
 }
 
 // ---------------- sun march: render.frag:75-142 ----------------
@@ -134,7 +129,7 @@ __device__ __forceinline__ uint32_t texel(const KernelArgs &a, int x, int y, int
 // by sdf_dir (0: R "up" for r.z > 0, 1: G "down").  Returns "lit"
 // (step == MAX_STEPS, render.frag:234).
 template <int CH>
-__device__ bool march_fast(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2,
+__device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int c1, int c2, float f0, float f1, float f2,
                            unsigned &fetches) {
     const FrameConsts &F = a.fc;
     const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
@@ -167,7 +162,7 @@ __device__ bool march_fast(const KernelArgs &a, int c0, int c1, int c2, float f0
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;                             // :120
         if ((unsigned)c0 >= (unsigned)a.X || (unsigned)c1 >= (unsigned)a.Y || (unsigned)c2 >= (unsigned)a.Z)
             return true;                                                          // :123-126 sky
-        const uint32_t t = texel(a, c0, c1, c2);                                  // :128
+        const uint32_t t = texel(fb, a, c0, c1, c2);                                  // :128
         fetches++;
         safe = CH == 0 ? (float)(t & 0xffu) : (float)((t >> 8) & 0xffu);
         step++;
@@ -177,7 +172,7 @@ __device__ bool march_fast(const KernelArgs &a, int c0, int c1, int c2, float f0
 
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
-__device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2,
+__device__ bool march_literal(const KernelArgs &a, const uint32_t *fb, int c0, int c1, int c2, float f0, float f1, float f2,
                               unsigned &fetches) {
     const FrameConsts &F = a.fc;
     const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
@@ -205,7 +200,7 @@ __device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float
         c0 += f2i(fl0); c1 += f2i(fl1); c2 += f2i(fl2);
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;
         if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) return true;
-        const uint32_t t = texel(a, c0, c1, c2);
+        const uint32_t t = texel(fb, a, c0, c1, c2);
         fetches++;
         safe = (float)((t >> sh) & 0xffu);
         step++;
@@ -216,10 +211,10 @@ __device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float
 // ---------------- primary visibility ----------------
 // First in-grid colour change along the view ray = the nearest front face of
 // the greedy mesh of sdf.cpp:281-356 after back-face culling.  Box-exit
-// stepping (oracle/vxo_render.c vxo_primary): the A byte R of a cell says the
-// box c +- R is air, so one step goes to the face where the ray leaves that
-// box (R = 0: an exact DDA step).  Returns 0 sky, 1 surface, 2 glass + what
-// is behind.
+// stepping (oracle/vxo_render.c vxo_primary): in the ray octant's field copy
+// the A byte R of a cell says the cube [c, c + R*s] ahead of it is air, so
+// one step goes to the face where the ray leaves that cube (R = 0: an exact
+// DDA step).  Returns 0 sky, 1 surface, 2 glass + what is behind.
 //
 // The loop runs on camera-relative cells held as fp32 integers (exact: the
 // host keeps |cam_cell| < 2^22), with x and y in packed-fp32 pairs:
@@ -228,10 +223,13 @@ __device__ bool march_literal(const KernelArgs &a, int c0, int c1, int c2, float
 //   crossing    tb = (A - o) * iv                                   (= oracle)
 //   exit axis   next h = A + s; others med3(floor(o + te*d) + hp, h - R, h + R)
 // d == 0 is a positive axis with iv = +inf: A - o >= 1 - o > 0 (0 <= o < 1 is
-// checked by vx_render), so tb = +inf exactly as the oracle's.
+// checked by vx_render), so tb = +inf exactly as the oracle's.  The cube
+// [c, c + R*s] lies ahead of the ray: clamp range [h, h + R] on a positive
+// axis, [h - R, h] on a negative one, i.e. [fma(hp - 1, R, h), fma(hp, R, h)].
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &g0, Surf &g1, Counters &cnt) {
+__device__ int primary(const KernelArgs &a, const uint32_t *fpad, float d0, float d1, float d2, Surf &g0, Surf &g1,
+                       Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
     const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
@@ -260,18 +258,17 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
     const int ip0 = p0, ip1 = p1, ip2 = p2;
     const f2 sxy = {p0 ? 1.0f : -1.0f, p1 ? 1.0f : -1.0f};
     const float sz = p2 ? 1.0f : -1.0f;
-    const f2 hpxy = {(float)ip0, (float)ip1};
-    const float hpz = (float)ip2;
+    const f2 hpxy = {(float)ip0, (float)ip1}, hmxy = {(float)(ip0 - 1), (float)(ip1 - 1)};
+    const float hpz = (float)ip2, hmz = (float)(ip2 - 1);
     const f2 oxy = {o0, o1}, dxy = {d0, d1}, ivxy = {iv0, iv1};
     f2 hxy = {(float)(c0 + ip0), (float)(c1 + ip1)};
     float hz = (float)(c2 + ip2);
     // padded index of h: kray + hx + Xp*hy + XpYp*hz, mod 2^32 with 24-bit
     // signed products (|h| < 2^23)
     const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
-    const __amdgpu_buffer_rsrc_t rs = field_rsrc_padded(a);
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
-        return __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)idx * 4u, 0, 0);
+        return fpad[(unsigned)idx];
     };
     uint32_t t = fetch(hxy.x, hxy.y, hz);
     cnt.prim_fetch++;
@@ -302,12 +299,12 @@ __device__ int primary(const KernelArgs &a, float d0, float d1, float d2, Surf &
         const f2 fxy = {floorf(pxy.x), floorf(pxy.y)};
         const f2 qxy = fxy + hpxy;
         const float qz = floorf(pz) + hpz;
-        const f2 loxy = hxy - Rv, hixy = hxy + Rv;
+        const f2 loxy = __builtin_elementwise_fma(hmxy, Rv, hxy), hixy = __builtin_elementwise_fma(hpxy, Rv, hxy);
         const f2 xxy = Axy + sxy;
         const float xz = Az + sz;
         const float n0 = e0 ? xxy.x : __builtin_amdgcn_fmed3f(qxy.x, loxy.x, hixy.x);
         const float n1 = e1 ? xxy.y : __builtin_amdgcn_fmed3f(qxy.y, loxy.y, hixy.y);
-        const float n2 = e2 ? xz : __builtin_amdgcn_fmed3f(qz, hz - R, hz + R);
+        const float n2 = e2 ? xz : __builtin_amdgcn_fmed3f(qz, __builtin_fmaf(hmz, R, hz), __builtin_fmaf(hpz, R, hz));
         hxy = (f2){n0, n1};
         hz = n2;
         hax = e0 ? 0 : (e1 ? 1 : 2);
@@ -378,17 +375,17 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
 }
 
 // sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G at LOD 0.
-__device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
+__device__ float sdf_lin(const KernelArgs &a, const uint32_t *fb, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
     const FrameConsts &F = a.fc;
     int x0, x1, y0, y1, z0, z1;
     float wx, wy, wz;
     lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
-    const uint32_t t000 = texel(a, x0, y0, z0), t100 = texel(a, x1, y0, z0);
-    const uint32_t t010 = texel(a, x0, y1, z0), t110 = texel(a, x1, y1, z0);
-    const uint32_t t001 = texel(a, x0, y0, z1), t101 = texel(a, x1, y0, z1);
-    const uint32_t t011 = texel(a, x0, y1, z1), t111 = texel(a, x1, y1, z1);
+    const uint32_t t000 = texel(fb, a, x0, y0, z0), t100 = texel(fb, a, x1, y0, z0);
+    const uint32_t t010 = texel(fb, a, x0, y1, z0), t110 = texel(fb, a, x1, y1, z0);
+    const uint32_t t001 = texel(fb, a, x0, y0, z1), t101 = texel(fb, a, x1, y0, z1);
+    const uint32_t t011 = texel(fb, a, x0, y1, z1), t111 = texel(fb, a, x1, y1, z1);
     float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
@@ -486,7 +483,7 @@ __device__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, flo
 }
 
 // ---------------- render.frag main(), block branch (render.frag:148-176, 207-251) ----------------
-__device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt) {
+__device__ void shade_block(const KernelArgs &a, const uint32_t *fb, const float *unorm, const Surf &g, float o[4], Counters &cnt) {
     const FrameConsts &F = a.fc;
     const int ni = g.nidx;
     const float n0 = ni == 0 ? 1.0f : (ni == 1 ? -1.0f : 0.0f);
@@ -501,7 +498,7 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
     float amb0 = 1.0f, amb1 = 1.0f, amb2 = 1.0f;
     if (!(F.flags & VX_FLAG_NO_AO)) {                                                  // :223-225
         cnt.ao++;
-        const float ambDist = sdf_lin(a, unorm, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
+        const float ambDist = sdf_lin(a, fb, unorm, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
         const float ambFactor = gmin(1.0f - sqrtf(ambDist), 0.8f);
         amb0 = gmix(1.0f, F.shadeCol[0], ambFactor);
         amb1 = gmix(1.0f, F.shadeCol[1], ambFactor);
@@ -512,10 +509,10 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
         cnt.shadow_rays++;
         bool lit;
         if (F.march_fast)
-            lit = F.sun_up ? march_fast<0>(a, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch)
-                           : march_fast<1>(a, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+            lit = F.sun_up ? march_fast<0>(a, fb, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch)
+                           : march_fast<1>(a, fb, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
         else
-            lit = march_literal(a, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+            lit = march_literal(a, fb, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
         shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
     }
     const float l0 = F.shadeCol[0] + 0.4f * shadeFactor;                               // :238
@@ -614,8 +611,12 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
     if (px < a.w && py < a.h) {
         float d0, d1, d2;
         view_ray(F, px, py, d0, d1, d2);
+        // the field copy of this ray's octant (zero components count positive)
+        const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
+        const uint32_t *fpad = a.field + (size_t)oct * a.copy_texels;
+        const uint32_t *fb = fpad + a.k0;
         Surf g[2];
-        const int n = primary(a, d0, d1, d2, g[0], g[1], cnt);
+        const int n = primary(a, fpad, d0, d1, d2, g[0], g[1], cnt);
         float rgba[4];
         if (F.flags & VX_FLAG_PRIMARY_ONLY) {
             primary_only_colour(n, g[0], rgba);
@@ -626,11 +627,11 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
             n_sky = 1;
             shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
-            shade_block(a, s_unorm, g[0], rgba, cnt);
+            shade_block(a, fb, s_unorm, g[0], rgba, cnt);
             if (g[0].id == 2) {
                 n_glass = 1;
                 float dst[4];
-                if (n == 2) shade_block(a, s_unorm, g[1], dst, cnt);
+                if (n == 2) shade_block(a, fb, s_unorm, g[1], dst, cnt);
                 else shade_sky(a, s_unorm, d0, d1, d2, dst, cnt);
                 const float al = rgba[3];
 #pragma unroll
@@ -679,44 +680,40 @@ __global__ void k_detile(const T *tiles, T *frame, int w, int h, int ts, int til
     if (x < w && y < h) frame[(size_t)y * w + x] = tiles[i];
 }
 
-// ---- A channel: half-size R = D - 1 of the air box around a cell, D the capped
-// Chebyshev distance to the nearest non-air cell (0 for non-air cells) ----
-__global__ void k_dist_x(const uint32_t *field, uint8_t *g1, int X, int Y, int Z, int cap) {
+// ---- A channel of octant copy `oct`: size r of the air cube ahead of a cell
+// (oracle vxo_field_octant), separable one-sided passes:
+// L = min_dz max(dz, min_dy max(dy, min_dx dx)), dx, dy, dz in [0, cap) toward
+// the octant, cells outside the grid air; r = L - 1 (0 for non-air) ----
+__global__ void k_oct_x(const uint32_t *field, uint8_t *g1, int X, int Y, int Z, int cap, int sx) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t N = (size_t)X * Y * Z;
-    if (i >= N) return;
+    if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X);
-    const size_t row = i - x;
     int best = cap;
     for (int k = 0; k < cap; k++) {
-        const int xa = x - k, xb = x + k;
-        if ((xa >= 0 && (field[row + xa] & 0x00ff0000u)) || (xb < X && (field[row + xb] & 0x00ff0000u))) {
-            best = k;
-            break;
-        }
+        const int xx = x + k * sx;
+        if (xx < 0 || xx >= X) break;
+        if ((field[i + (ptrdiff_t)(k * sx)] >> 16) & 0xff) { best = k; break; }
     }
     g1[i] = (uint8_t)best;
 }
-__global__ void k_dist_yz(const uint8_t *gin, uint8_t *gout, uint32_t *field, int X, int Y, int Z, int cap, int axis) {
+
+__global__ void k_oct_yz(const uint8_t *gin, uint8_t *gout, uint32_t *field, int X, int Y, int Z, int cap, int axis,
+                         int sgn) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t N = (size_t)X * Y * Z;
-    if (i >= N) return;
-    const int y = (int)((i / X) % Y);
-    const int z = (int)(i / ((size_t)X * Y));
-    const int pos = axis == 1 ? y : z, n = axis == 1 ? Y : Z;
-    const size_t stride = axis == 1 ? (size_t)X : (size_t)X * Y;
-    const size_t base = i - (size_t)pos * stride;
+    if (i >= (size_t)X * Y * Z) return;
+    const int pos = axis == 1 ? (int)((i / X) % Y) : (int)(i / ((size_t)X * Y));
+    const int n = axis == 1 ? Y : Z;
+    const ptrdiff_t stride = axis == 1 ? (ptrdiff_t)X : (ptrdiff_t)X * Y;
     int best = cap;
-    const int lo = pos - (cap - 1) < 0 ? 0 : pos - (cap - 1);
-    const int hi = pos + (cap - 1) > n - 1 ? n - 1 : pos + (cap - 1);
-    for (int q = lo; q <= hi; q++) {
-        const int v = gin[base + (size_t)q * stride];
-        const int ak = q > pos ? q - pos : pos - q;
-        const int m = v > ak ? v : ak;
+    for (int k = 0; k < cap; k++) {
+        const int q = pos + k * sgn;
+        if (q < 0 || q >= n) break;
+        const int v = gin[(ptrdiff_t)i + (ptrdiff_t)(k * sgn) * stride];
+        const int m = v > k ? v : k;
         best = m < best ? m : best;
     }
     if (axis == 1) gout[i] = (uint8_t)best;
-    else field[i] = (field[i] & 0x00ffffffu) | ((uint32_t)(best > 0 ? best - 1 : 0) << 24);   // A = R
+    else field[i] = (field[i] & 0x00ffffffu) | ((uint32_t)(best > 0 ? best - 1 : 0) << 24);
 }
 
 __global__ void k_reduce_stats(unsigned long long *stats) {
@@ -791,13 +788,15 @@ int launch_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, in
     return (int)hipGetLastError();
 }
 
-int launch_field_dist(uint32_t *field, int X, int Y, int Z, int cap, uint8_t *ga, uint8_t *gb, void *stream) {
+int launch_field_octant(uint32_t *field, int X, int Y, int Z, int cap, int oct, uint8_t *ga, uint8_t *gb,
+                        void *stream) {
     const size_t N = (size_t)X * Y * Z;
     dim3 grid((unsigned)((N + 255) / 256)), block(256);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_dist_x, grid, block, 0, s, field, ga, X, Y, Z, cap);
-    hipLaunchKernelGGL(k_dist_yz, grid, block, 0, s, ga, gb, field, X, Y, Z, cap, 1);
-    hipLaunchKernelGGL(k_dist_yz, grid, block, 0, s, gb, ga, field, X, Y, Z, cap, 2);
+    const int sx = oct & 1 ? -1 : 1, sy = oct & 2 ? -1 : 1, sz = oct & 4 ? -1 : 1;
+    hipLaunchKernelGGL(k_oct_x, grid, block, 0, s, (const uint32_t *)field, ga, X, Y, Z, cap, sx);
+    hipLaunchKernelGGL(k_oct_yz, grid, block, 0, s, ga, gb, field, X, Y, Z, cap, 1, sy);
+    hipLaunchKernelGGL(k_oct_yz, grid, block, 0, s, gb, ga, field, X, Y, Z, cap, 2, sz);
     return (int)hipGetLastError();
 }
 

@@ -141,10 +141,11 @@ class Scene:
     def __exit__(self, *exc):
         self.close()
 
-    def read_field(self) -> np.ndarray:
+    def read_field(self, octant: int = 0) -> np.ndarray:
+        """(Z, Y, X, 4) RGBA8 of the device field copy for ray octant ``octant``."""
         X, Y, Z = self.dims
         out = np.empty((Z, Y, X, 4), np.uint8)
-        check(lib().vx_scene_read_field(self.handle, out.ctypes.data, out.nbytes))
+        check(lib().vx_scene_read_field_copy(self.handle, octant, out.ctypes.data, out.nbytes))
         return out
 
     def render(self, frame: Frame, *, pixel_format=_abi.PIXEL_RGBA32F, stats: bool = False):
