@@ -128,6 +128,12 @@ __device__ __forceinline__ uint32_t texel(const uint32_t *fb, const KernelArgs &
 // component, so no 0*inf NaN; every t finite and < 1025).  CH = channel read
 // by sdf_dir (0: R "up" for r.z > 0, 1: G "down").  Returns "lit"
 // (step == MAX_STEPS, render.frag:234).
+//
+// Loop shape: one exit test per step (sky, safe == 0 or the step budget),
+// cells kept as exact fp32 integers, the three-way min and its tie test as
+// min3/med3 (two or more axes share the minimum iff med3 == min3, then the
+// literal length of render.frag:105-116), and a sky lane's load redirected to
+// cell 0 instead of branching around it.
 template <int CH>
 __device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int c1, int c2, float f0, float f1, float f2,
                            unsigned &fetches) {
@@ -137,9 +143,11 @@ __device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int 
     const float y0 = F.sun_rcp[0], y1 = F.sun_rcp[1], y2 = F.sun_rcp[2];
     const float r0 = F.sun[0], r1 = F.sun[1], r2 = F.sun[2];
     const int maxs = F.max_steps;
+    if (maxs <= 0) return maxs == 0;
     float safe = 1.0f;
-    int step = 0;
-    while (step < maxs && safe != 0.0f) {
+    float e0 = (float)c0, e1 = (float)c1, e2 = (float)c2;
+    int step = 0;                                                                // wave-uniform
+    do {
         const float x0 = -f0 * s0, x1 = -f1 * s1, x2 = -f2 * s2;                  // :94
         const float d0 = (x0 - floorf(x0)) + 1e-4f;
         const float d1 = (x1 - floorf(x1)) + 1e-4f;
@@ -147,27 +155,28 @@ __device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int 
         const float t0 = div_const(d0, b0, y0);                                  // :97
         const float t1 = div_const(d1, b1, y1);
         const float t2 = div_const(d2, b2, y2);
-        const float m12 = __builtin_fminf(t1, t2), m20 = __builtin_fminf(t2, t0), m01 = __builtin_fminf(t0, t1);
-        const bool m0 = t0 <= m12, m1 = t1 <= m20, m2 = t2 <= m01;              // :100-104
-        float len = __builtin_fminf(t0, m12);                                    // :105, one axis
-        if ((int)m0 + (int)m1 + (int)m2 > 1) {                                   // ties: literal length
-            const float v0 = m0 ? t0 : 0.0f, v1 = m1 ? t1 : 0.0f, v2 = m2 ? t2 : 0.0f;
+        float len = __builtin_fminf(__builtin_fminf(t0, t1), t2);               // :100-105, one axis
+        if (__builtin_amdgcn_fmed3f(t0, t1, t2) == len) {                        // ties: literal length
+            const float v0 = t0 == len ? t0 : 0.0f, v1 = t1 == len ? t1 : 0.0f, v2 = t2 == len ? t2 : 0.0f;
             len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
         }
         f0 = f0 + (r0 * safe) * len;                                             // :118
         f1 = f1 + (r1 * safe) * len;
         f2 = f2 + (r2 * safe) * len;
         const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
-        c0 += (int)fl0; c1 += (int)fl1; c2 += (int)fl2;                          // :119
+        e0 += fl0; e1 += fl1; e2 += fl2;                                         // :119 (exact)
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;                             // :120
-        if ((unsigned)c0 >= (unsigned)a.X || (unsigned)c1 >= (unsigned)a.Y || (unsigned)c2 >= (unsigned)a.Z)
-            return true;                                                          // :123-126 sky
-        const uint32_t t = texel(fb, a, c0, c1, c2);                                  // :128
-        fetches++;
-        safe = CH == 0 ? (float)(t & 0xffu) : (float)((t >> 8) & 0xffu);
-        step++;
-    }
-    return step == maxs;
+        const int i0 = (int)e0, i1 = (int)e1, i2 = (int)e2;
+        const bool sky = (unsigned)i0 >= (unsigned)a.X || (unsigned)i1 >= (unsigned)a.Y || (unsigned)i2 >= (unsigned)a.Z;
+        const unsigned idx = (unsigned)i0 + __umul24((unsigned)a.Xp, (unsigned)i1) + __umul24(a.XpYp, (unsigned)i2);
+        const uint32_t t = fb[sky ? 0u : idx];                                   // :123-128
+        fetches += sky ? 0u : 1u;
+        // safe < 0 marks "lit": left the grid (:123-126), or the step that
+        // reaches MAX_STEPS, whatever it read (:234 tests step, not safe)
+        safe = sky ? -1.0f : (CH == 0 ? (float)(t & 0xffu) : (float)((t >> 8) & 0xffu));
+        if (++step >= maxs) safe = -1.0f;
+    } while (safe > 0.0f);
+    return safe < 0.0f;
 }
 
 // Literal path for any other sun direction (zero or tiny components: the
