@@ -40,7 +40,9 @@ struct vx_scene {
     int device = 0;
     int X = 0, Y = 0, Z = 0;
     int noise_w = 0, noise_h = 0;
-    uint32_t *d_field = nullptr;
+    uint16_t *d_prim = nullptr;   // 8 padded octant copies (vx_internal.h FieldLayout)
+    uint8_t *d_sun = nullptr;     // R, G channels
+    uint16_t *d_rg = nullptr;     // R | G << 8
     uint32_t *d_noise = nullptr;
     unsigned long long *d_stats = nullptr;
     int *d_tiles = nullptr;
@@ -50,7 +52,7 @@ struct vx_scene {
     std::vector<int> h_tiles, h_detile;   // last lists uploaded to d_tiles / d_detile
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    FieldLayout L;  // d_field is padded (vx_internal.h)
+    FieldLayout L;
 };
 
 #define VX_HIP(call)                                                                                 \
@@ -109,8 +111,8 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     if (cap < 1 || cap > 255) return set_error(VX_EINVAL, "dist_cap must be in [1,255]");
     const FieldLayout L = field_layout(X, Y, Z, cap);
     // 32-bit buffer byte offsets and 24-bit index products in the kernels
-    if (L.texels * 4ull >= (1ull << 31) || (unsigned long long)L.Xp * L.Yp >= (1ull << 23))
-        return set_error(VX_EINVAL, "vx_scene_create: field too large (padded field must be < 2 GiB)");
+    if (L.texels >= (1ull << 31) || (unsigned long long)L.Xp * L.Yp >= (1ull << 23))
+        return set_error(VX_EINVAL, "vx_scene_create: field too large (padded grid must be < 2^31 cells)");
     if ((NW & (NW - 1)) || (NH & (NH - 1))) return set_error(VX_EINVAL, "noise dims must be powers of two");
     if (!!d->map_path == !!d->map_bytes) return set_error(VX_EINVAL, "set exactly one of map_path / map_bytes");
     const size_t field_bytes = (size_t)X * Y * Z * 4, noise_bytes = (size_t)NW * NH * 4;
@@ -136,40 +138,41 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     auto fail = [&](int code) { vx_scene_destroy(s); return code; };
     hipError_t e;
     uint8_t *ga = nullptr, *gb = nullptr;
+    uint32_t *lin = nullptr;   // the linear RGBA upload, A rewritten per octant
     if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
-        (e = hipMalloc(&s->d_field, field_bytes)) != hipSuccess ||
+        (e = hipMalloc(&lin, field_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
-        (e = hipMemcpyAsync(s->d_field, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(lin, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(s->d_noise, noise.data(), noise_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) {
         if (ga) (void)hipFree(ga);
         if (gb) (void)hipFree(gb);
+        if (lin) (void)hipFree(lin);
         return fail(set_error(VX_EDEVICE, std::string("scene upload failed: ") + hipGetErrorString(e)));
     }
-    // 8 octant copies in the padded layout: each copy's A
-    // channel is computed in place in the linear upload, then scattered into
-    // the copy, whose border keeps the out-of-grid sentinel
-    uint32_t *copies = nullptr;
+    // the kernels' arrays: sun channels and AO array from
+    // the upload, then per octant its cube sizes into the upload's A channel
+    // and from there into that octant's prim copy (border = sentinel)
+    const size_t N = (size_t)X * Y * Z;
     int lrc = 0;
-    if ((e = hipMalloc(&copies, 8 * L.texels * 4)) == hipSuccess &&
-        (e = hipMemsetD32Async((hipDeviceptr_t)copies, 0xFF000000u, 8 * L.texels, s->stream)) == hipSuccess) {
+    if ((e = hipMalloc(&s->d_prim, 8 * L.texels * 2)) == hipSuccess &&
+        (e = hipMalloc(&s->d_sun, 2 * N)) == hipSuccess && (e = hipMalloc(&s->d_rg, 2 * N)) == hipSuccess &&
+        (e = hipMemsetD16Async((hipDeviceptr_t)s->d_prim, 0xFF00u, 8 * L.texels, s->stream)) == hipSuccess) {
+        lrc = launch_field_pack(lin, nullptr, s->d_sun, s->d_rg, X, Y, Z, L.pad, s->stream);
         for (int oct = 0; oct < 8 && !lrc; oct++) {
-            lrc = launch_field_octant(s->d_field, X, Y, Z, cap, oct, ga, gb, s->stream);
-            if (!lrc) lrc = launch_field_pad(s->d_field, copies + oct * L.texels, X, Y, Z, L.pad, 1, s->stream);
+            lrc = launch_field_octant(lin, X, Y, Z, cap, oct, ga, gb, s->stream);
+            if (!lrc) lrc = launch_field_pack(lin, s->d_prim + oct * L.texels, nullptr, nullptr, X, Y, Z, L.pad, s->stream);
         }
         e = hipStreamSynchronize(s->stream);
     }
     (void)hipFree(ga);
     (void)hipFree(gb);
-    if (lrc != 0 || e != hipSuccess) {
-        if (copies) (void)hipFree(copies);
+    (void)hipFree(lin);
+    if (lrc != 0 || e != hipSuccess)
         return fail(set_error(VX_EDEVICE, std::string("field preparation failed: ") +
                                               hipGetErrorString(lrc ? (hipError_t)lrc : e)));
-    }
-    (void)hipFree(s->d_field);
-    s->d_field = copies;
     s->L = L;
     *out = s;
     return VX_OK;
@@ -179,7 +182,9 @@ void vx_scene_destroy(vx_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    if (s->d_field) (void)hipFree(s->d_field);
+    if (s->d_prim) (void)hipFree(s->d_prim);
+    if (s->d_sun) (void)hipFree(s->d_sun);
+    if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
@@ -206,8 +211,8 @@ int vx_scene_read_field_copy(vx_scene *s, int octant, void *host_out, size_t cap
     VX_HIP(hipSetDevice(s->device));
     uint32_t *lin = nullptr;
     VX_HIP(hipMalloc(&lin, n));
-    hipError_t e = (hipError_t)launch_field_pad(s->d_field + (size_t)octant * s->L.texels, lin, s->X, s->Y, s->Z,
-                                                 s->L.pad, 0, s->stream);
+    hipError_t e = (hipError_t)launch_field_unpack(s->d_rg, s->d_prim + (size_t)octant * s->L.texels, lin, s->X, s->Y,
+                                                   s->Z, s->L.pad, s->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, lin, n, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(lin);
@@ -257,7 +262,9 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     KernelArgs a;
     std::memset(&a, 0, sizeof a);
-    a.field = s->d_field;
+    a.prim = s->d_prim;
+    a.sun = s->d_sun;
+    a.rg = s->d_rg;
     a.noise = s->d_noise;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;
     a.noise_w = s->noise_w; a.noise_h = s->noise_h;
@@ -272,7 +279,8 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
     a.Xp = s->L.Xp;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
-    a.k0 = (unsigned)s->L.k0;
+    a.XY = (unsigned)s->X * (unsigned)s->Y;
+    a.XYZ = a.XY * (unsigned)s->Z;
     a.copy_texels = (unsigned)s->L.texels;
     a.kcam = (unsigned)(p->cam_cell[0] + s->L.pad) + (unsigned)a.Xp * (unsigned)(p->cam_cell[1] + s->L.pad) +
              a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);   // mod 2^32

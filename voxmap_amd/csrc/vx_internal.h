@@ -37,7 +37,9 @@ struct FrameConsts {
 
 // Parameters of one render launch (passed by value to the kernel).
 struct KernelArgs {
-    const uint32_t *field;   // 8 octant copies of the padded field (FieldLayout)
+    const uint16_t *prim;    // 8 padded octant copies: colour | cube size << 8 (FieldLayout)
+    const uint8_t *sun;      // R channel then G channel, X*Y*Z bytes each
+    const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *noise;   // RGBA8 noise texels
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
@@ -52,8 +54,8 @@ struct KernelArgs {
     int max_shadow_steps;
     int Xp;                  // padded row length (FieldLayout)
     unsigned XpYp;           // padded slice size
-    unsigned k0;             // padded index of grid cell (0, 0, 0)
-    unsigned copy_texels;    // texels per octant copy (FieldLayout::texels)
+    unsigned XY, XYZ;        // X*Y, X*Y*Z
+    unsigned copy_texels;    // cells per prim copy (FieldLayout::texels)
     unsigned kcam;           // padded index of the camera cell, mod 2^32
     FrameConsts fc;
 };
@@ -65,17 +67,21 @@ enum StatSlot {
     ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_COUNT
 };
 
-// Field layout in HBM: 8 copies, one per ray octant, each the
-// X x Y x Z grid (x fastest, as map.bin; A = the octant's air-cube size)
-// inside a border of pad = cap sentinel texels on every side.
+// Field data in HBM (vx_kernels.hip): `prim` = 8 copies (one
+// per ray octant) of the X x Y x Z grid, u16 colour | air-cube size << 8,
+// inside a border of pad = cap sentinel cells; `sun` = R and G channels (u8);
+// `rg` = R | G << 8 (u16).
 struct FieldLayout {
     int pad, Xp, Yp, Zp;
-    size_t texels;           // Xp * Yp * Zp, one copy
-    size_t k0;               // index of grid cell (0, 0, 0)
+    size_t texels;           // Xp * Yp * Zp, one prim copy
 };
 FieldLayout field_layout(int X, int Y, int Z, int cap);
-// linear grid <-> padded field; to_padded = 1 scatters src into dst
-int launch_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, int pad, int to_padded, void *stream);
+// linear RGBA upload (A = an octant's cube sizes) -> prim copy; -> sun, rg (either may be null)
+int launch_field_pack(const uint32_t *lin, uint16_t *prim_copy, uint8_t *sun, uint16_t *rg, int X, int Y, int Z,
+                      int pad, void *stream);
+// RGBA of one octant copy, linear
+int launch_field_unpack(const uint16_t *rg, const uint16_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
+                        void *stream);
 
 // Launchers (vx_kernels.hip).  Return a hipError_t as int.
 int launch_render(const KernelArgs &a, int pixel_format, void *stream);

@@ -107,20 +107,22 @@ struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
 };
 
-// Field in HBM: 8 copies, one per octant of ray directions, each the
-// reference's x-fastest texels (R, G, B as map.bin) with A = the octant's
-// air-cube size, inside a border of P = cap sentinel cells (A = 255, never a
-// real value: A <= cap - 1 <= 254), so the primary traversal detects leaving
-// the grid from the texel it loads.  A pixel reads only its primary ray's
-// copy.  Every read is in bounds: the traversal stays within P of the grid,
-// march() returns before reading outside it, the AO sample clamps.
-constexpr uint32_t kSentinel = 0xFF000000u;
+// Field data in HBM, each array shaped for the loop that
+// reads it, so a cache line holds as many useful cells as possible:
+//   prim  8 copies, one per ray octant, u16 per cell: colour | air-cube size
+//         << 8, inside a border of P = cap sentinel cells (0xFF00: size 255,
+//         never real, sizes are <= cap - 1 <= 254), so the primary traversal
+//         detects leaving the grid from the value it loads;
+//   sun   map.bin's R ("up") and G ("down") channels, u8 each, linear: the
+//         sun march reads one of them;
+//   rg    R | G << 8, u16, linear: the AO trilinear sample.
+// Every read is in bounds: the traversal stays within P of the grid, march()
+// returns before reading outside it, the AO sample clamps.
+constexpr uint32_t kSentinel = 0xFF00u;
 
-// fb = the pixel's copy at grid cell (0, 0, 0); Xp < 2^16 and XpYp < 2^23
-// (vx_scene_create), so full-rate 24-bit multiplies.
-__device__ __forceinline__ uint32_t texel(const uint32_t *fb, const KernelArgs &a, int x, int y, int z) {
-    const unsigned idx = (unsigned)x + __umul24((unsigned)a.Xp, (unsigned)y) + __umul24(a.XpYp, (unsigned)z);
-    return fb[idx];
+// x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
+__device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
+    return (unsigned)x + __umul24((unsigned)a.X, (unsigned)y) + __umul24(a.XY, (unsigned)z);
 }
 
 // ---------------- sun march: render.frag:75-142 ----------------
@@ -134,8 +136,8 @@ __device__ __forceinline__ uint32_t texel(const uint32_t *fb, const KernelArgs &
 // min3/med3 (two or more axes share the minimum iff med3 == min3, then the
 // literal length of render.frag:105-116), and a sky lane's load redirected to
 // cell 0 instead of branching around it.
-template <int CH>
-__device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int c1, int c2, float f0, float f1, float f2,
+template <int CH>   // CH: documents the channel; the caller passes its array
+__device__ bool march_fast(const KernelArgs &a, const uint8_t *sun, int c0, int c1, int c2, float f0, float f1, float f2,
                            unsigned &fetches) {
     const FrameConsts &F = a.fc;
     const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
@@ -168,12 +170,11 @@ __device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int 
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;                             // :120
         const int i0 = (int)e0, i1 = (int)e1, i2 = (int)e2;
         const bool sky = (unsigned)i0 >= (unsigned)a.X || (unsigned)i1 >= (unsigned)a.Y || (unsigned)i2 >= (unsigned)a.Z;
-        const unsigned idx = (unsigned)i0 + __umul24((unsigned)a.Xp, (unsigned)i1) + __umul24(a.XpYp, (unsigned)i2);
-        const uint32_t t = fb[sky ? 0u : idx];                                   // :123-128
+        const uint32_t t = sun[sky ? 0u : lin_index(a, i0, i1, i2)];             // :123-128
         fetches += sky ? 0u : 1u;
         // safe < 0 marks "lit": left the grid (:123-126), or the step that
         // reaches MAX_STEPS, whatever it read (:234 tests step, not safe)
-        safe = sky ? -1.0f : (CH == 0 ? (float)(t & 0xffu) : (float)((t >> 8) & 0xffu));
+        safe = sky ? -1.0f : (float)t;
         if (++step >= maxs) safe = -1.0f;
     } while (safe > 0.0f);
     return safe < 0.0f;
@@ -181,7 +182,7 @@ __device__ bool march_fast(const KernelArgs &a, const uint32_t *fb, int c0, int 
 
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
-__device__ bool march_literal(const KernelArgs &a, const uint32_t *fb, int c0, int c1, int c2, float f0, float f1, float f2,
+__device__ bool march_literal(const KernelArgs &a, const uint8_t *sun, int c0, int c1, int c2, float f0, float f1, float f2,
                               unsigned &fetches) {
     const FrameConsts &F = a.fc;
     const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
@@ -209,9 +210,9 @@ __device__ bool march_literal(const KernelArgs &a, const uint32_t *fb, int c0, i
         c0 += f2i(fl0); c1 += f2i(fl1); c2 += f2i(fl2);
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;
         if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) return true;
-        const uint32_t t = texel(fb, a, c0, c1, c2);
+        const uint32_t t = sun[lin_index(a, c0, c1, c2)];
         fetches++;
-        safe = (float)((t >> sh) & 0xffu);
+        safe = (float)t;
         step++;
     }
     return step == maxs;
@@ -237,7 +238,7 @@ __device__ bool march_literal(const KernelArgs &a, const uint32_t *fb, int c0, i
 // axis, [h - R, h] on a negative one, i.e. [fma(hp - 1, R, h), fma(hp, R, h)].
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ int primary(const KernelArgs &a, const uint32_t *fpad, float d0, float d1, float d2, Surf &g0, Surf &g1,
+__device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, float d1, float d2, Surf &g0, Surf &g1,
                        Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
@@ -277,12 +278,12 @@ __device__ int primary(const KernelArgs &a, const uint32_t *fpad, float d0, floa
     const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
-        return fpad[(unsigned)idx];
+        return (uint32_t)ppad[(unsigned)idx];
     };
     uint32_t t = fetch(hxy.x, hxy.y, hz);
     cnt.prim_fetch++;
-    int prev = (t >> 16) & 0xff;
-    float R = (float)(t >> 24);
+    int prev = t & 0xff;
+    float R = (float)(t >> 8);
     // ints, not bools: loop-carried and live-out lane masks cost SALU merges per step
     int have_glass = 0, stop;
     f2 gxy = {0.0f, 0.0f};
@@ -321,7 +322,7 @@ __device__ int primary(const KernelArgs &a, const uint32_t *fpad, float d0, floa
         t = fetch(n0, n1, n2);
         const bool oob = t >= kSentinel;               // left the grid: sky behind
         cnt.prim_fetch += oob ? 0u : 1u;
-        col = (t >> 16) & 0xff;
+        col = t & 0xff;
         const bool change = col != prev && !oob;
         const bool gfirst = change && col == kGlass && have_glass == 0;
         if (gfirst) {                                  // glass: blend over the next surface
@@ -331,7 +332,7 @@ __device__ int primary(const KernelArgs &a, const uint32_t *fpad, float d0, floa
         stop = (oob || (change && !gfirst)) ? 1 : 0;
         asm volatile("" : "+v"(stop));
         prev = col;
-        R = (float)(t >> 24);
+        R = (float)(t >> 8);
     } while (stop == 0 && ++it < cap);
     asm volatile("" : "+v"(col));
     if (stop == 0) cnt.cap_hit++;
@@ -384,17 +385,17 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
 }
 
 // sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G at LOD 0.
-__device__ float sdf_lin(const KernelArgs &a, const uint32_t *fb, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
+__device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
     const FrameConsts &F = a.fc;
     int x0, x1, y0, y1, z0, z1;
     float wx, wy, wz;
     lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
-    const uint32_t t000 = texel(fb, a, x0, y0, z0), t100 = texel(fb, a, x1, y0, z0);
-    const uint32_t t010 = texel(fb, a, x0, y1, z0), t110 = texel(fb, a, x1, y1, z0);
-    const uint32_t t001 = texel(fb, a, x0, y0, z1), t101 = texel(fb, a, x1, y0, z1);
-    const uint32_t t011 = texel(fb, a, x0, y1, z1), t111 = texel(fb, a, x1, y1, z1);
+    const uint32_t t000 = (uint32_t)a.rg[lin_index(a, x0, y0, z0)], t100 = (uint32_t)a.rg[lin_index(a, x1, y0, z0)];
+    const uint32_t t010 = (uint32_t)a.rg[lin_index(a, x0, y1, z0)], t110 = (uint32_t)a.rg[lin_index(a, x1, y1, z0)];
+    const uint32_t t001 = (uint32_t)a.rg[lin_index(a, x0, y0, z1)], t101 = (uint32_t)a.rg[lin_index(a, x1, y0, z1)];
+    const uint32_t t011 = (uint32_t)a.rg[lin_index(a, x0, y1, z1)], t111 = (uint32_t)a.rg[lin_index(a, x1, y1, z1)];
     float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
@@ -492,7 +493,7 @@ __device__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, flo
 }
 
 // ---------------- render.frag main(), block branch (render.frag:148-176, 207-251) ----------------
-__device__ void shade_block(const KernelArgs &a, const uint32_t *fb, const float *unorm, const Surf &g, float o[4], Counters &cnt) {
+__device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt) {
     const FrameConsts &F = a.fc;
     const int ni = g.nidx;
     const float n0 = ni == 0 ? 1.0f : (ni == 1 ? -1.0f : 0.0f);
@@ -507,7 +508,7 @@ __device__ void shade_block(const KernelArgs &a, const uint32_t *fb, const float
     float amb0 = 1.0f, amb1 = 1.0f, amb2 = 1.0f;
     if (!(F.flags & VX_FLAG_NO_AO)) {                                                  // :223-225
         cnt.ao++;
-        const float ambDist = sdf_lin(a, fb, unorm, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
+        const float ambDist = sdf_lin(a, unorm, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
         const float ambFactor = gmin(1.0f - sqrtf(ambDist), 0.8f);
         amb0 = gmix(1.0f, F.shadeCol[0], ambFactor);
         amb1 = gmix(1.0f, F.shadeCol[1], ambFactor);
@@ -518,10 +519,10 @@ __device__ void shade_block(const KernelArgs &a, const uint32_t *fb, const float
         cnt.shadow_rays++;
         bool lit;
         if (F.march_fast)
-            lit = F.sun_up ? march_fast<0>(a, fb, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch)
-                           : march_fast<1>(a, fb, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+            lit = F.sun_up ? march_fast<0>(a, a.sun, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch)
+                           : march_fast<1>(a, a.sun + a.XYZ, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
         else
-            lit = march_literal(a, fb, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+            lit = march_literal(a, F.sun_up ? a.sun : a.sun + a.XYZ, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
         shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
     }
     const float l0 = F.shadeCol[0] + 0.4f * shadeFactor;                               // :238
@@ -622,10 +623,8 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
         view_ray(F, px, py, d0, d1, d2);
         // the field copy of this ray's octant (zero components count positive)
         const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
-        const uint32_t *fpad = a.field + (size_t)oct * a.copy_texels;
-        const uint32_t *fb = fpad + a.k0;
         Surf g[2];
-        const int n = primary(a, fpad, d0, d1, d2, g[0], g[1], cnt);
+        const int n = primary(a, a.prim + (size_t)oct * a.copy_texels, d0, d1, d2, g[0], g[1], cnt);
         float rgba[4];
         if (F.flags & VX_FLAG_PRIMARY_ONLY) {
             primary_only_colour(n, g[0], rgba);
@@ -636,11 +635,11 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
             n_sky = 1;
             shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
-            shade_block(a, fb, s_unorm, g[0], rgba, cnt);
+            shade_block(a, s_unorm, g[0], rgba, cnt);
             if (g[0].id == 2) {
                 n_glass = 1;
                 float dst[4];
-                if (n == 2) shade_block(a, fb, s_unorm, g[1], dst, cnt);
+                if (n == 2) shade_block(a, s_unorm, g[1], dst, cnt);
                 else shade_sky(a, s_unorm, d0, d1, d2, dst, cnt);
                 const float al = rgba[3];
 #pragma unroll
@@ -767,15 +766,32 @@ int launch_detile(const void *tiles, void *frame, int w, int h, int ts, int tile
 }
 
 namespace {
-// linear x-fastest grid <-> the padded field (border cells keep the sentinel)
-__global__ void k_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, int P, int to_padded) {
+// linear RGBA upload (A = one octant's cube sizes) -> that octant's prim copy
+__global__ void k_pack_prim(const uint32_t *src, uint16_t *dst, int X, int Y, int Z, int P) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
     const size_t Xp = (size_t)X + 2 * P, Yp = (size_t)Y + 2 * P;
-    const size_t j = (size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P));
-    if (to_padded) dst[j] = src[i];
-    else dst[i] = src[j];
+    const uint32_t t = src[i];
+    dst[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))] = (uint16_t)(((t >> 16) & 0xffu) | ((t >> 24) << 8));
+}
+// linear RGBA upload -> sun channel arrays and the AO array
+__global__ void k_pack_sun(const uint32_t *src, uint8_t *sun, uint16_t *rg, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const uint32_t t = src[i];
+    sun[i] = (uint8_t)(t & 0xffu);
+    sun[N + i] = (uint8_t)((t >> 8) & 0xffu);
+    rg[i] = (uint16_t)(t & 0xffffu);
+}
+// RGBA of one octant copy (R, G from rg; B, A from prim) for vx_scene_read_field_copy
+__global__ void k_unpack(const uint16_t *rg, const uint16_t *prim, uint32_t *dst, int X, int Y, int Z, int P) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)X * Y * Z) return;
+    const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+    const size_t Xp = (size_t)X + 2 * P, Yp = (size_t)Y + 2 * P;
+    const uint32_t p = prim[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))];
+    dst[i] = (uint32_t)rg[i] | ((p & 0xffu) << 16) | ((p >> 8) << 24);
 }
 }  // namespace
 
@@ -786,14 +802,23 @@ FieldLayout field_layout(int X, int Y, int Z, int cap) {
     L.Yp = Y + 2 * cap;
     L.Zp = Z + 2 * cap;
     L.texels = (size_t)L.Xp * L.Yp * L.Zp;
-    L.k0 = (size_t)cap * (1 + (size_t)L.Xp + (size_t)L.Xp * L.Yp);
     return L;
 }
 
-int launch_field_pad(const uint32_t *src, uint32_t *dst, int X, int Y, int Z, int pad, int to_padded, void *stream) {
+int launch_field_pack(const uint32_t *lin, uint16_t *prim_copy, uint8_t *sun, uint16_t *rg, int X, int Y, int Z,
+                      int pad, void *stream) {
     const size_t N = (size_t)X * Y * Z;
-    hipLaunchKernelGGL(k_field_pad, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, src, dst, X,
-                       Y, Z, pad, to_padded);
+    const dim3 grid((unsigned)((N + 255) / 256)), block(256);
+    if (prim_copy) hipLaunchKernelGGL(k_pack_prim, grid, block, 0, (hipStream_t)stream, lin, prim_copy, X, Y, Z, pad);
+    if (sun) hipLaunchKernelGGL(k_pack_sun, grid, block, 0, (hipStream_t)stream, lin, sun, rg, N);
+    return (int)hipGetLastError();
+}
+
+int launch_field_unpack(const uint16_t *rg, const uint16_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
+                        void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, prim_copy,
+                       out, X, Y, Z, pad);
     return (int)hipGetLastError();
 }
 
