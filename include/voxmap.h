@@ -71,7 +71,7 @@ typedef struct vx_scene_desc {
     int noise_w, noise_h;       /* 0 -> 1024 x 1024 (render.js:141) */
     int X, Y, Z;                /* 0 -> 1024, 256, 32 (render.h:14-16) */
     int device;                 /* HIP device ordinal */
-    int dist_cap;               /* A-channel distance cap, 0 -> 32 */
+    int dist_cap;               /* air-cube size cap of the primary traversal (and border width), 0 -> 32 */
     uint32_t noise_seed;        /* seed of the synthetic noise when none is given */
 } vx_scene_desc;
 

@@ -1,2 +1,1 @@
-bash tools/gpu_check.sh && bash tools/ablate.sh && \
-TAG=full bash tools/pmc.sh "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
+TAG=r01 bash tools/profile.sh && timeout -k 10 300 python bench.py > gpurun_out/bench_full.log 2>&1; tail -1 gpurun_out/bench_full.log
