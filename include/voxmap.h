@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 1
+#define VX_ABI_VERSION 2
 
 /* error codes */
 #define VX_OK 0
@@ -51,6 +51,14 @@ extern "C" {
 #define VX_FLAG_NO_CLOUDS 0x4u   /* sky without noise fetches (render.frag:181-203) */
 #define VX_FLAG_PRIMARY_ONLY 0x8u /* primary visibility only: v_color of the first surface
                                     (render.vert:30), sky = palette(0); BASELINE config C1 */
+/* Extensions (BASELINE "full quality" = shadow + reflection +
+ * clouds + rough normals).  The reference has no code for them (README.md:15-22
+ * describes an earlier renderer's reflections and rough normals, README.md:56-57
+ * lists soft shadows as to-do); DESIGN.md §3 "Extensions" defines them. */
+#define VX_FLAG_REFLECT 0x10u    /* glass mirrors the traced scene (Fresnel-weighted) */
+#define VX_FLAG_ROUGH 0x20u      /* shading normal jittered by white() noise (render.frag:21) */
+#define VX_FLAG_FULL_QUALITY (VX_FLAG_REFLECT | VX_FLAG_ROUGH)
+#define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;
 
@@ -92,6 +100,9 @@ typedef struct vx_frame_params {
     float ray_up[3];
     uint32_t flags;             /* VX_FLAG_* */
     int max_shadow_steps;       /* MAX_STEPS (render.frag:12); <= 0 -> 2*Z */
+    int shadow_samples;         /* ext soft shadows: <= 1 the reference's hard shadow,
+                                   2..VX_MAX_SHADOW_SAMPLES sun-disc samples (vx_sun_samples) */
+    float sun_radius;           /* ext: sun-disc radius (tangent-plane, radians) for the samples */
 } vx_frame_params;
 
 /* Counters of the work one vx_render call did (algorithmic). */
@@ -101,7 +112,10 @@ typedef struct vx_stats {
     uint64_t shadow_rays, shadow_fetches;
     uint64_t ao_samples, noise_px;
     uint64_t primary_cap_hits;  /* must be 0 */
-    uint64_t alg_bytes;         /* 4*fetches + 32*ao + 80*sky + out bytes */
+    uint64_t reflect_rays, reflect_fetches;   /* ext REFLECT: reflection rays traced, texels read */
+    uint64_t rough_px;          /* ext ROUGH: fragments with a jittered normal (4 noise texels each) */
+    uint64_t alg_bytes;         /* 4*(primary+shadow+reflect fetches) + 32*ao + 80*clouded sky
+                                   + 16*rough + out bytes */
     double kernel_ms;           /* HIP-event time of the render kernel(s) */
 } vx_stats;
 
@@ -146,6 +160,9 @@ int vx_frame_from_orbit(const double sbj[3], const double rot[3], int w, int h, 
 int vx_frame_from_matrix(const float u_matrix[16], const double cam_pos[3], vx_frame_params *p);
 /* map.js:399-402: hour -> sun direction. */
 void vx_sun_from_hour(double hour, float sun[3]);
+/* The soft-shadow sun directions a frame with shadow_samples = n uses
+ * (DESIGN.md §3): n <= 1 -> the sun itself; n is clamped to 16. */
+int vx_sun_samples(const float sun[3], float radius, int n, float out[][3]);
 
 /* Decode a field/asset container to raw bytes (render.js:52-58). */
 int vx_decode(const void *in, size_t n, int format, const char *key_jwk_k,

@@ -28,7 +28,8 @@ class OScene(C.Structure):
 class OStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("pixels", "sky_px", "block_px", "glass_px", "primary_fetches",
                                           "shadow_rays", "shadow_fetches", "ao_samples", "noise_px",
-                                          "primary_cap_hits")]
+                                          "primary_cap_hits", "reflect_rays", "reflect_fetches",
+                                          "rough_px")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -69,6 +70,8 @@ def lib():
         L.vxo_shade.argtypes = [C.POINTER(OScene), C.c_void_p, C.POINTER(OGbuf), C.POINTER(C.c_float),
                                 C.POINTER(C.c_float), C.c_void_p]
         L.vxo_pixel_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+        L.vxo_sun_samples.argtypes = [C.POINTER(C.c_float), C.c_float, C.c_int, C.POINTER(C.c_float)]
+        L.vxo_sun_samples.restype = None
         L.vxo_exp2.argtypes = [C.c_float]
         L.vxo_exp2.restype = C.c_float
         L.vxo_field_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -138,6 +141,15 @@ def field_octant(field_zyx4: np.ndarray, oct: int, cap: int = 32) -> np.ndarray:
     Z, Y, X, _ = f.shape
     out = np.empty((Z, Y, X), np.uint8)
     lib().vxo_field_octant(f.ctypes.data, X, Y, Z, cap, oct, out.ctypes.data)
+    return out
+
+
+def sun_samples(sun, radius: float, n: int) -> np.ndarray:
+    """(max(n,1), 3) float32 soft-shadow sun directions (vxo_sun_samples)."""
+    m = max(1, min(int(n), 16))
+    out = np.zeros((m, 3), np.float32)
+    lib().vxo_sun_samples((C.c_float * 3)(*sun), float(radius), int(n),
+                          out.ctypes.data_as(C.POINTER(C.c_float)))
     return out
 
 

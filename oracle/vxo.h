@@ -52,7 +52,15 @@ typedef struct {
     float ray_up[3];
     unsigned flags;
     int max_shadow_steps;     /* MAX_STEPS = 2*Z (render.frag:12); <=0 -> 2*Z */
+    int shadow_samples;       /* ext (README "Soft shadows"): <=1 hard, 2..16 sun samples */
+    float sun_radius;         /* ext: angular radius of the sun disc, radians */
 } vxo_frame;
+
+/* Extension flags (no reference code exists for them, so the
+ * build defines them — DESIGN.md §3 "Extensions"): */
+#define VXO_FLAG_REFLECT 0x10u  /* glass reflects the traced scene (README.md:15-20) */
+#define VXO_FLAG_ROUGH 0x20u    /* per-fragment normal jitter from white() (README.md:22, render.frag:21) */
+#define VXO_MAX_SAMPLES 16
 
 typedef struct {
     uint64_t pixels, sky_px, block_px, glass_px;
@@ -60,6 +68,8 @@ typedef struct {
     uint64_t shadow_rays, shadow_fetches;
     uint64_t ao_samples, noise_px;
     uint64_t primary_cap_hits; /* primary marches that hit the iteration cap */
+    uint64_t reflect_rays, reflect_fetches;  /* ext REFLECT: traced reflection rays, texels */
+    uint64_t rough_px;         /* ext ROUGH: fragments whose normal was jittered */
 } vxo_stats;
 
 /* march() result (render.frag:64-70) */
@@ -103,6 +113,11 @@ void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
 
 /* Per-pixel ray direction for pixel (px,py) (float, fixed op order). */
 void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3]);
+
+/* Soft-shadow sun directions (ext): n samples of the sun disc of angular
+ * radius `radius` around sun (Vogel spiral, double precision, rounded to
+ * float).  n <= 1 gives the sun itself. */
+void vxo_sun_samples(const float sun[3], float radius, int n, float out[][3]);
 
 /* Deterministic transcendental used by both oracle and kernel. */
 float vxo_exp2(float x);

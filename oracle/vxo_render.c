@@ -181,6 +181,25 @@ static float fbm(const vxo_scene *s, float px, float py) {
     return 1.0f - 2.0f * t;
 }
 
+/* white(p) = noise(p).rgb = 1 - 2*texture(u_noise, p).rgb (render.frag:16-21),
+ * same bilinear REPEAT LOD-0 filter as fbm().  Used by the ROUGH extension. */
+static void white(const vxo_scene *s, float px, float py, float out[3]) {
+    const int W = s->noise_w, H = s->noise_h;
+    float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
+    float fu = floorf(u), fv = floorf(v);
+    float a = u - fu, b = v - fv;
+    int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
+    int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+    for (int ch = 0; ch < 3; ch++) {
+        float t00 = unorm(s->noise[4 * ((size_t)y0 * W + x0) + ch]);
+        float t10 = unorm(s->noise[4 * ((size_t)y0 * W + x1) + ch]);
+        float t01 = unorm(s->noise[4 * ((size_t)y1 * W + x0) + ch]);
+        float t11 = unorm(s->noise[4 * ((size_t)y1 * W + x1) + ch]);
+        float r0 = g_mix(t00, t10, a), r1 = g_mix(t01, t11, a);
+        out[ch] = 1.0f - 2.0f * g_mix(r0, r1, b);
+    }
+}
+
 /* ---------------- march() (render.frag:75-142), literally ---------------- */
 void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
                const float r[3], int max_steps, vxo_march_t *res) {
@@ -248,41 +267,22 @@ static inline int in_grid(const vxo_scene *s, const int a[3]) {
     return a[0] >= 0 && a[1] >= 0 && a[2] >= 0 && a[0] < s->X && a[1] < s->Y && a[2] < s->Z;
 }
 
-int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
-                vxo_gbuf g[2], int *fetches, int *cap_hit) {
+/* Octant-cube walk of the ray B + o + t*d (B an integer cell, camera- or
+ * origin-relative cells c) from the start cell B + c to the first colour
+ * change.  glass_layer != 0: a glass entry is recorded and the walk goes on to
+ * the next change behind it (primary visibility); 0: the first change ends
+ * the walk (reflection rays).  A start cell outside the grid is sky. */
+static int walk(const vxo_scene *s, const int cc[3], const float o[3], const float d[3], int c[3],
+                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit) {
     const int dims[3] = {s->X, s->Y, s->Z};
-    const float *o = f->cam_fract;
-    const int *cc = f->cam_cell;
     float inv[3];
     int stp[3];
-    float tlo = 0.0f, thi = INFINITY;
-    *fetches = 0;
-    *cap_hit = 0;
-    for (int i = 0; i < 3; i++) {        /* ray / grid AABB */
-        stp[i] = d[i] > 0.0f ? 1 : -1;
-        float lo = (float)(0 - cc[i]) - o[i];
-        float hi = (float)(dims[i] - cc[i]) - o[i];
-        if (d[i] != 0.0f) {
-            inv[i] = 1.0f / d[i];
-            float t0 = lo * inv[i], t1 = hi * inv[i];
-            if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
-            tlo = g_max(tlo, t0);
-            thi = g_min(thi, t1);
-        } else {
-            inv[i] = 0.0f;
-            if (!(lo <= 0.0f && 0.0f < hi)) return 0;
-        }
-    }
-    if (!(tlo < thi)) return 0;
-
-    int c[3];                            /* camera-relative cell */
     for (int i = 0; i < 3; i++) {
-        float p = o[i] + tlo * d[i];
-        int ci = g_f2i(floorf(p));
-        int lo = -cc[i], hi = dims[i] - cc[i] - 1;
-        c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
+        stp[i] = d[i] > 0.0f ? 1 : -1;
+        inv[i] = d[i] != 0.0f ? 1.0f / d[i] : 0.0f;
     }
     int abs_c[3] = {c[0] + cc[0], c[1] + cc[1], c[2] + cc[2]};
+    if (!in_grid(s, abs_c)) return 0;
     const uint8_t *tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
     (*fetches)++;
     const int oct = (d[0] < 0.0f ? 1 : 0) | (d[1] < 0.0f ? 2 : 0) | (d[2] < 0.0f ? 4 : 0);
@@ -329,7 +329,7 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
                 }
             }
             nrec++;
-            if (h->id != 2 || nrec == 2) return nrec;
+            if (!glass_layer || h->id != 2 || nrec == 2) return nrec;
         }
         prev = col;
     }
@@ -338,21 +338,146 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
 #undef OCT_R
 }
 
+int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
+                vxo_gbuf g[2], int *fetches, int *cap_hit) {
+    const int dims[3] = {s->X, s->Y, s->Z};
+    const float *o = f->cam_fract;
+    const int *cc = f->cam_cell;
+    float tlo = 0.0f, thi = INFINITY;
+    *fetches = 0;
+    *cap_hit = 0;
+    for (int i = 0; i < 3; i++) {        /* ray / grid AABB */
+        float lo = (float)(0 - cc[i]) - o[i];
+        float hi = (float)(dims[i] - cc[i]) - o[i];
+        if (d[i] != 0.0f) {
+            float inv = 1.0f / d[i];
+            float t0 = lo * inv, t1 = hi * inv;
+            if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
+            tlo = g_max(tlo, t0);
+            thi = g_min(thi, t1);
+        } else {
+            if (!(lo <= 0.0f && 0.0f < hi)) return 0;
+        }
+    }
+    if (!(tlo < thi)) return 0;
+
+    int c[3];                            /* camera-relative cell */
+    for (int i = 0; i < 3; i++) {
+        float p = o[i] + tlo * d[i];
+        int ci = g_f2i(floorf(p));
+        int lo = -cc[i], hi = dims[i] - cc[i] - 1;
+        c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
+    }
+    return walk(s, cc, o, d, c, 1, g, fetches, cap_hit);
+}
+
 void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3]) {
     float nx = (float)(2 * px + 1) / (float)w - 1.0f;
     float ny = 1.0f - (float)(2 * py + 1) / (float)h;
     for (int i = 0; i < 3; i++) d[i] = (f->ray_fwd[i] + nx * f->ray_right[i]) + ny * f->ray_up[i];
 }
 
-/* ---------------- main() (render.frag:147-252) ---------------- */
+/* ---------------- extensions (DESIGN.md §3 "Extensions") -------
+ * The reference has no code for these (README.md:15-22 describes reflections
+ * and rough normals of an earlier renderer, :56-57 lists soft shadows as to-do);
+ * the definitions below are this build's, shared with the kernel. */
+
+/* cos/sin of k * golden angle, k = 0..15 (Vogel spiral) as double literals,
+ * so no libm trigonometry enters the sample directions. */
+static const double VOGEL_CS[VXO_MAX_SAMPLES][2] = {
+    {1.0, 0.0},
+    {-0.7373688780783197, 0.6754902942615238},
+    {0.08742572471695988, -0.9961710408648278},
+    {0.6084388609788626, 0.7936007512916959},
+    {-0.9847134853154287, -0.17418195037931164},
+    {0.8437552948123972, -0.5367280526263227},
+    {-0.25960430490148856, 0.9657150743757783},
+    {-0.4609070247133692, -0.8874484292452546},
+    {0.9393212963241181, 0.343038630874102},
+    {-0.9243455561378048, 0.38155640847493627},
+    {0.4238459950479107, -0.9057342725556136},
+    {0.2992838644448729, 0.954164120307897},
+    {-0.86521120975323, -0.5014075812324265},
+    {0.976675773628176, -0.21471942904125782},
+    {-0.5751294291397393, 0.8180624302199665},
+    {-0.12851068979899324, -0.9917081236973845},
+};
+
+/* Soft-shadow directions: sample k of n is the sun direction pushed by
+ * radius * sqrt((k + 0.5) / n) along the spiral angle of k in the plane
+ * normal to the sun (basis u = normalize(a x sun), v = sun x u with
+ * a = z unless the sun is within ~25 degrees of it, then x), normalised;
+ * double precision (+ - * / sqrt only), rounded to float. */
+void vxo_sun_samples(const float sun[3], float radius, int n, float out[][3]) {
+    if (n <= 1) {
+        out[0][0] = sun[0]; out[0][1] = sun[1]; out[0][2] = sun[2];
+        return;
+    }
+    if (n > VXO_MAX_SAMPLES) n = VXO_MAX_SAMPLES;
+    const double sd[3] = {sun[0], sun[1], sun[2]};
+    const double ax[3] = {fabs(sd[2]) < 0.9 ? 0.0 : 1.0, 0.0, fabs(sd[2]) < 0.9 ? 1.0 : 0.0};
+    double u[3] = {ax[1] * sd[2] - ax[2] * sd[1], ax[2] * sd[0] - ax[0] * sd[2], ax[0] * sd[1] - ax[1] * sd[0]};
+    const double ul = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    u[0] /= ul; u[1] /= ul; u[2] /= ul;
+    const double v[3] = {sd[1] * u[2] - sd[2] * u[1], sd[2] * u[0] - sd[0] * u[2], sd[0] * u[1] - sd[1] * u[0]};
+    for (int k = 0; k < n; k++) {
+        const double r = (double)radius * sqrt(((double)k + 0.5) / (double)n);
+        const double cu = r * VOGEL_CS[k][0], cv = r * VOGEL_CS[k][1];
+        double x[3];
+        for (int i = 0; i < 3; i++) x[i] = sd[i] + cu * u[i] + cv * v[i];
+        const double l = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+        for (int i = 0; i < 3; i++) out[k][i] = (float)(x[i] / l);
+    }
+}
+
+#define ROUGH_SCALE 0.00390625f   /* 1/256: 4 noise texels per voxel on a 1024 texture */
+#define ROUGH_AMP 0.1f
+
+/* ROUGH: the shading normal of a face fragment is normalize(n + 0.1 * white(p))
+ * with p the fragment's two in-face coordinates (axes other than the face
+ * axis, in increasing order) times 1/256. */
+static void rough_normal(const vxo_scene *s, const vxo_gbuf *g, const float n[3], float out[3]) {
+    const int a = g->normal_idx >> 1;
+    const int t1 = a == 0 ? 1 : 0, t2 = a == 2 ? 1 : 2;
+    const float u = (float)g->cell[t1] + g->fract[t1], v = (float)g->cell[t2] + g->fract[t2];
+    float w[3], m[3];
+    white(s, u * ROUGH_SCALE, v * ROUGH_SCALE, w);
+    for (int i = 0; i < 3; i++) m[i] = n[i] + ROUGH_AMP * w[i];
+    float l = sqrtf(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+    out[0] = m[0] / l; out[1] = m[1] / l; out[2] = m[2] / l;
+}
+
+/* Per-frame state derived once (the kernel's FrameConsts play this role). */
+typedef struct {
+    const vxo_scene *s;
+    const vxo_frame *f;
+    int max_steps;
+    int n_sun;                               /* >= 2: soft shadows */
+    float sun_dirs[VXO_MAX_SAMPLES][3];
+} shade_ctx;
+
+static void ctx_init(shade_ctx *c, const vxo_scene *s, const vxo_frame *f) {
+    c->s = s;
+    c->f = f;
+    c->max_steps = f->max_shadow_steps > 0 ? f->max_shadow_steps : 2 * s->Z;
+    c->n_sun = f->shadow_samples > 1 ? (f->shadow_samples > VXO_MAX_SAMPLES ? VXO_MAX_SAMPLES : f->shadow_samples) : 1;
+    vxo_sun_samples(f->sun_dir, f->sun_radius, c->n_sun, c->sun_dirs);
+}
+
+/* ---------------- main() (render.frag:147-252) ----------------
+ * ray: NULL = the camera ray to the fragment (:154); for sky records the
+ * direction to normalise (the skybox is at infinity); for surfaces seen in a
+ * reflection the (unit) reflected ray.  ray_used receives rayDir. */
 static inline float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 static void normalize3(const float v[3], float out[3]) {
     float l = sqrtf(dot3(v, v));
     out[0] = v[0] / l; out[1] = v[1] / l; out[2] = v[2] / l;
 }
 
-void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
-               const float prim_dir[3], float o_color[4], vxo_stats *st) {
+static void shade_frag(const shade_ctx *c, const vxo_gbuf *g, const float ray[3], float o_color[4],
+                       float ray_used[3], vxo_stats *st) {
+    const vxo_scene *s = c->s;
+    const vxo_frame *f = c->f;
     o_color[0] = 0.0f; o_color[1] = 0.0f; o_color[2] = 0.0f; o_color[3] = 1.0f;    /* :148 */
     const int isSky = g->id == 1, isGlass = g->id == 2;                            /* :150-151 */
     const float litCol[3] = {0.4f, 0.35f, 0.3f};                                   /* :153 */
@@ -361,17 +486,26 @@ void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
     palette(isSky ? 0 : g->color, v_color);
     float rayDir[3];
     if (isSky) {
-        normalize3(prim_dir, rayDir);   /* skybox modelled at infinity */
+        normalize3(ray, rayDir);        /* skybox modelled at infinity */
+    } else if (ray) {
+        rayDir[0] = ray[0]; rayDir[1] = ray[1]; rayDir[2] = ray[2];   /* ext REFLECT: reflected ray */
     } else {
         float v[3];
         for (int i = 0; i < 3; i++)
             v[i] = (float)(g->cell[i] - f->cam_cell[i]) + (g->fract[i] - f->cam_fract[i]);   /* :154 */
         normalize3(v, rayDir);
     }
+    if (ray_used) { ray_used[0] = rayDir[0]; ray_used[1] = rayDir[1]; ray_used[2] = rayDir[2]; }
+    /* ext ROUGH: shading normal; geometry (AO offset, march start) keeps v_normal */
+    float nrm[3] = {v_normal[0], v_normal[1], v_normal[2]};
+    if (!isSky && (f->flags & VXO_FLAG_ROUGH)) {
+        rough_normal(s, g, v_normal, nrm);
+        if (st) st->rough_px++;
+    }
     float reflectDir[3];                                                           /* :155 reflect() */
     {
-        float k = 2.0f * dot3(v_normal, rayDir);
-        for (int i = 0; i < 3; i++) reflectDir[i] = rayDir[i] - k * v_normal[i];
+        float k = 2.0f * dot3(nrm, rayDir);
+        for (int i = 0; i < 3; i++) reflectDir[i] = rayDir[i] - k * nrm[i];
     }
     const float *sunDir = f->sun_dir;                                              /* :157 */
     const float sunCol[3] = {1.4f, 1.0f, 0.5f};                                    /* :162 */
@@ -429,11 +563,11 @@ void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
     }
     /* block branch :207-251 */
     const float *baseCol = v_color;                                                 /* :209 */
-    float an[3] = {fabsf(v_normal[0]), fabsf(v_normal[1]), fabsf(v_normal[2])};
+    float an[3] = {fabsf(nrm[0]), fabsf(nrm[1]), fabsf(nrm[2])};
     const float M0[3] = {0.90f, 0.90f, 0.95f}, M1[3] = {0.95f, 0.95f, 1.00f}, M2[3] = {1.0f, 1.0f, 1.0f};
     float normalCol[3];
     for (int i = 0; i < 3; i++) normalCol[i] = (M0[i] * an[0] + M1[i] * an[1]) + M2[i] * an[2]; /* :211-215 */
-    if (v_normal[2] < 0.0f)                                                         /* :217 */
+    if (nrm[2] < 0.0f)                                                              /* :217 */
         for (int i = 0; i < 3; i++) normalCol[i] = normalCol[i] * 0.8f;
     float shadeCol[3];
     for (int i = 0; i < 3; i++) shadeCol[i] = 0.7f * scatterCol[i];                 /* :220 */
@@ -447,13 +581,22 @@ void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
         for (int i = 0; i < 3; i++) ambCol[i] = g_mix(1.0f, shadeCol[i], ambFactor); /* :225 */
     }
     float shadeFactor = f->sun_dir[2] < 0.0f ? 0.0f
-                        : sqrtf(g_max(0.0f, dot3(v_normal, f->sun_dir)));           /* :228-229 */
+                        : sqrtf(g_max(0.0f, dot3(nrm, f->sun_dir)));                /* :228-229 */
     if (shadeFactor > 0.0f && !(f->flags & 0x1u)) {  /* :232; VX_FLAG_NO_SHADOW skips */
-        const int max_steps = f->max_shadow_steps > 0 ? f->max_shadow_steps : 2 * s->Z;
         vxo_march_t sun;
-        vxo_march(s, g->cell, g->fract, sunDir, max_steps, &sun);                   /* :233 */
-        shadeFactor = shadeFactor * (sun.step == max_steps ? 1.0f : 0.0f);          /* :234 */
-        if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
+        if (c->n_sun <= 1) {
+            vxo_march(s, g->cell, g->fract, sunDir, c->max_steps, &sun);            /* :233 */
+            shadeFactor = shadeFactor * (sun.step == c->max_steps ? 1.0f : 0.0f);   /* :234 */
+            if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
+        } else {                 /* ext soft shadows: lit fraction of the sun samples */
+            int lit = 0;
+            for (int k = 0; k < c->n_sun; k++) {
+                vxo_march(s, g->cell, g->fract, c->sun_dirs[k], c->max_steps, &sun);
+                lit += sun.step == c->max_steps ? 1 : 0;
+                if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
+            }
+            shadeFactor = shadeFactor * ((float)lit / (float)c->n_sun);
+        }
     }
     float lightCol[3];
     for (int i = 0; i < 3; i++) lightCol[i] = shadeCol[i] + litCol[i] * shadeFactor; /* :238 */
@@ -461,15 +604,69 @@ void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
     if (f->quality > 0)                                                             /* :242-244 */
         for (int i = 0; i < 3; i++) o_color[i] = o_color[i] * ((normalCol[i] * lightCol[i]) * ambCol[i]);
     if (isGlass) {                                                                  /* :246-249 */
-        o_color[3] = 0.8f * vxo_exp2(dot3(rayDir, v_normal));
+        o_color[3] = 0.8f * vxo_exp2(dot3(rayDir, nrm));
         for (int i = 0; i < 3; i++) o_color[i] = o_color[i] * (0.2f * atmCol[i]);
     }
 }
 
+void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
+               const float prim_dir[3], float o_color[4], vxo_stats *st) {
+    shade_ctx c;
+    ctx_init(&c, s, f);
+    shade_frag(&c, g, g->id == 1 ? prim_dir : NULL, o_color, NULL, st);
+}
+
+static void sky_record(vxo_gbuf *sky) {
+    memset(sky, 0, sizeof *sky);
+    sky->id = 1;
+    sky->normal_idx = 1;
+}
+
+/* ext REFLECT: colour seen along the mirror reflection of the camera ray at a
+ * glass fragment (geometric normal: R = rayDir with the face-axis component
+ * negated, exactly reflect(rayDir, n)).  The ray starts on the face, in the
+ * cell on the camera's side, and walks the octant cubes to the first colour
+ * change; the surface found is shaded as a fragment seen along R (its own AO,
+ * sun march, rough normal; no further reflection), a miss is the sky along R. */
+static void reflect_color(const shade_ctx *c, const vxo_gbuf *gl, const float rd[3], float out[3],
+                          vxo_stats *st) {
+    const int a = gl->normal_idx >> 1;
+    float R[3] = {rd[0], rd[1], rd[2]};
+    R[a] = -R[a];
+    int B[3], c0[3];
+    float o[3];
+    for (int i = 0; i < 3; i++) {
+        if (i == a) {
+            B[i] = gl->cell[i];
+            o[i] = 0.0f;
+            c0[i] = R[i] > 0.0f ? 0 : -1;
+        } else {
+            const float fl = floorf(gl->fract[i]);
+            B[i] = gl->cell[i] + g_f2i(fl);
+            o[i] = gl->fract[i] - fl;
+            c0[i] = 0;
+        }
+    }
+    vxo_gbuf h[2];
+    int fetches = 0, cap_hit = 0;
+    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit);
+    if (st) { st->reflect_rays++; st->reflect_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
+    float rgba[4];
+    if (n == 0) {
+        vxo_gbuf sky;
+        sky_record(&sky);
+        shade_frag(c, &sky, R, rgba, NULL, st);
+    } else {
+        shade_frag(c, &h[0], R, rgba, NULL, st);
+    }
+    out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
+}
+
 /* One pixel: primary visibility, shading, glass blend (render.js:84-86
  * SRC_ALPHA / ONE_MINUS_SRC_ALPHA over the surface behind). */
-static void render_pixel(const vxo_scene *s, const vxo_frame *f, int w, int h, int px, int py,
-                         float out[4], vxo_stats *st) {
+static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float out[4], vxo_stats *st) {
+    const vxo_scene *s = c->s;
+    const vxo_frame *f = c->f;
     float d[3];
     vxo_pixel_dir(f, w, h, px, py, d);
     vxo_gbuf g[2];
@@ -477,9 +674,7 @@ static void render_pixel(const vxo_scene *s, const vxo_frame *f, int w, int h, i
     int n = vxo_primary(s, f, d, g, &fetches, &cap_hit);
     if (st) { st->pixels++; st->primary_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
     vxo_gbuf sky;
-    memset(&sky, 0, sizeof sky);
-    sky.id = 1;
-    sky.normal_idx = 1;
+    sky_record(&sky);
     if (f->flags & 0x8u) {   /* VX_FLAG_PRIMARY_ONLY: v_color of the first surface, sky = palette(0) */
         if (st) { if (n == 0) st->sky_px++; else if (g[0].id == 2) st->glass_px++; else st->block_px++; }
         palette(n == 0 ? 0 : g[0].color, out);
@@ -488,15 +683,26 @@ static void render_pixel(const vxo_scene *s, const vxo_frame *f, int w, int h, i
     }
     if (n == 0) {
         if (st) st->sky_px++;
-        vxo_shade(s, f, &sky, d, out, st);
+        shade_frag(c, &sky, d, out, NULL, st);
     } else if (g[0].id != 2) {
         if (st) st->block_px++;
-        vxo_shade(s, f, &g[0], d, out, st);
+        shade_frag(c, &g[0], NULL, out, NULL, st);
     } else {
         if (st) st->glass_px++;
-        float src[4], dst[4];
-        vxo_shade(s, f, &g[0], d, src, st);
-        vxo_shade(s, f, n == 2 ? &g[1] : &sky, d, dst, st);
+        float src[4], dst[4], rd[3];
+        shade_frag(c, &g[0], NULL, src, rd, st);
+        if (f->flags & VXO_FLAG_REFLECT) {
+            /* Schlick's Fresnel with F0 = 0.04 on the geometric normal:
+             * cos = |rayDir| along the face axis */
+            float refl[3];
+            reflect_color(c, &g[0], rd, refl, st);
+            const float cs = g_min(fabsf(rd[g[0].normal_idx >> 1]), 1.0f);
+            const float x = 1.0f - cs, x2 = x * x;
+            const float F = 0.04f + 0.96f * ((x2 * x2) * x);
+            for (int i = 0; i < 3; i++) src[i] = src[i] + F * refl[i];
+        }
+        if (n == 2) shade_frag(c, &g[1], NULL, dst, NULL, st);
+        else shade_frag(c, &sky, d, dst, NULL, st);
         float a = src[3];
         for (int i = 0; i < 3; i++) out[i] = src[i] * a + dst[i] * (1.0f - a);
     }
@@ -507,6 +713,8 @@ void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
                 int row0, int row_step, float *out, vxo_stats *st, int n_threads) {
     if (row_step <= 0) row_step = 1;
     int nrows = row0 < h ? (h - 1 - row0) / row_step + 1 : 0;
+    shade_ctx ctx;
+    ctx_init(&ctx, s, f);
     vxo_stats acc;
     memset(&acc, 0, sizeof acc);
 #ifdef _OPENMP
@@ -522,7 +730,7 @@ void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
         for (int k = 0; k < nrows; k++) {
             int py = row0 + k * row_step;
             for (int px = 0; px < w; px++)
-                render_pixel(s, f, w, h, px, py, out + 4 * ((size_t)py * w + px), &loc);
+                render_pixel(&ctx, w, h, px, py, out + 4 * ((size_t)py * w + px), &loc);
         }
 #ifdef _OPENMP
 #pragma omp critical

@@ -24,6 +24,11 @@ CASES = [
     {"name": "proc_top", "seed": 7, "dims": [96, 48, 16], "sbj": [48.0, 24.0, 40.0], "rot": [1e-4, 0.0, -0.002]},
     {"name": "proc_glass_grazing", "seed": 11, "dims": [128, 64, 24], "sbj": [-6.0, 32.0, 9.0],
      "rot": [1.45, 0.0, -1.5707963267948966], "n_glass": 12},
+    # extensions (pinned to this build's own definition only)
+    {"name": "ext_full_quality", "seed": 11, "dims": [128, 64, 24], "sbj": [-6.0, 32.0, 9.0],
+     "rot": [1.45, 0.0, -1.5707963267948966], "n_glass": 12, "frame": {"flags": 48}},
+    {"name": "ext_soft16", "seed": 5, "dims": [96, 48, 16], "sbj": [48.0, 24.0, 18.0], "rot": [1.1, 0.0, 0.6],
+     "frame": {"flags": 48, "shadow_samples": 16, "sun_radius": 0.05}},
 ]
 W, H = 64, 48
 
@@ -32,7 +37,7 @@ def inputs(case):
     g = scenes.small_proc(case["seed"], dims=tuple(case["dims"]), n_boxes=16, n_glass=case.get("n_glass", 6))
     field = vx.field_build(g)
     noise = vx.noise_synth(0)
-    fr = vx.make_frame(tuple(case["sbj"]), tuple(case["rot"]), W, H)
+    fr = vx.make_frame(tuple(case["sbj"]), tuple(case["rot"]), W, H, **case.get("frame", {}))
     return field, noise, fr
 
 

@@ -193,3 +193,55 @@ def test_campus_scene(noise):
         img, _ = sc.render(fr)
     ref, _ = oracle.Oracle(dev_field, noise).render(fr.params, 480, 270, threads=16)
     _compare(img, ref)
+
+
+# ---- extensions: REFLECT, ROUGH, soft shadows -------------------
+EXT_CASES = {
+    "reflect": dict(flags=0x10),
+    "rough": dict(flags=0x20),
+    "full_quality": dict(flags=0x30),
+    "soft8": dict(shadow_samples=8, sun_radius=0.05),
+    "soft16_full": dict(flags=0x30, shadow_samples=16, sun_radius=0.04),
+    "soft_sun_low": dict(shadow_samples=6, sun_radius=0.3, sun=(0.9, 0.3, 0.05)),   # samples below the horizon
+    "soft_axis_zero": dict(shadow_samples=4, sun_radius=0.0, sun=(0.6, 0.0, 0.8)),  # literal march per sample
+    "full_no_ao_no_clouds": dict(flags=0x30 | 0x2 | 0x4),
+}
+
+
+@pytest.mark.parametrize("case", list(EXT_CASES))
+@pytest.mark.parametrize("seed,dims,sbj,rot", SMALL[:2] + SMALL[3:])
+def test_extensions_bit_exact(seed, dims, sbj, rot, noise, case):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    grid = scenes.small_proc(seed, dims=dims, n_boxes=16, n_glass=10)
+    field = vx.field_build(grid)
+    fr = vx.make_frame(sbj, rot, 160, 96, **EXT_CASES[case])
+    with _scene(vx, field, noise, dims) as sc:
+        dev_field = sc.read_field()
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, 160, 96)
+    _compare(img, ref)
+    g, o = st.as_dict(), ost.as_dict()
+    for k in o:
+        assert g[k] == o[k], (k, g[k], o[k])
+    assert st.primary_cap_hits == 0
+
+
+@pytest.mark.parametrize("cfg,cam,step,kw", [
+    ("C3", "K1", 41, dict(flags=0x30)),                                   # BASELINE C3 "full quality"
+    ("C2", "K2", 17, dict(flags=0x30, shadow_samples=4, sun_radius=0.03)),
+])
+def test_extensions_baseline_rows(full_scene, noise, cfg, cam, step, kw):
+    import oracle
+    from voxmap_amd import presets
+    sc, dev_field = full_scene
+    c = presets.CONFIGS[cfg]
+    fr = presets.camera_frame(cam, c["w"], c["h"], **kw)
+    img, st = sc.render(fr, stats=True)
+    ref, _ = oracle.Oracle(dev_field, noise).render(fr.params, c["w"], c["h"], row0=step // 2, row_step=step,
+                                                    threads=16)
+    rows = np.arange(step // 2, c["h"], step)
+    _compare(img, ref, rows)
+    assert st.primary_cap_hits == 0
+    assert st.reflect_rays == st.glass_px

@@ -24,6 +24,10 @@ ERROR_NAMES = {
 FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB = 0, 1, 2, 3
 PIXEL_RGBA32F, PIXEL_RGBA8 = 0, 1
 FLAG_NO_SHADOW, FLAG_NO_AO, FLAG_NO_CLOUDS, FLAG_PRIMARY_ONLY = 0x1, 0x2, 0x4, 0x8
+FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
+FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
+MAX_SHADOW_SAMPLES = 16
+ABI_VERSION = 2
 
 
 class SceneDesc(C.Structure):
@@ -44,6 +48,7 @@ class FrameParams(C.Structure):
         ("cam_cell", C.c_int * 3), ("cam_fract", C.c_float * 3), ("sun_dir", C.c_float * 3),
         ("ray_fwd", C.c_float * 3), ("ray_right", C.c_float * 3), ("ray_up", C.c_float * 3),
         ("flags", C.c_uint32), ("max_shadow_steps", C.c_int),
+        ("shadow_samples", C.c_int), ("sun_radius", C.c_float),
     ]
 
     def copy(self) -> "FrameParams":
@@ -57,6 +62,7 @@ class Stats(C.Structure):
         ("pixels", C.c_uint64), ("sky_px", C.c_uint64), ("block_px", C.c_uint64), ("glass_px", C.c_uint64),
         ("primary_fetches", C.c_uint64), ("shadow_rays", C.c_uint64), ("shadow_fetches", C.c_uint64),
         ("ao_samples", C.c_uint64), ("noise_px", C.c_uint64), ("primary_cap_hits", C.c_uint64),
+        ("reflect_rays", C.c_uint64), ("reflect_fetches", C.c_uint64), ("rough_px", C.c_uint64),
         ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double),
     ]
 
@@ -82,6 +88,7 @@ SIGNATURES = [
                                       C.POINTER(FrameParams)]),
     ("vx_frame_from_matrix", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(FrameParams)]),
     ("vx_sun_from_hour", None, [C.c_double, C.POINTER(C.c_float)]),
+    ("vx_sun_samples", C.c_int, [C.POINTER(C.c_float), C.c_float, C.c_int, C.POINTER(C.c_float)]),
     ("vx_decode", C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_char_p, C.c_void_p, C.c_size_t,
                             C.POINTER(C.c_size_t)]),
     ("vx_blob_encrypt", C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, C.c_void_p, C.c_size_t,

@@ -236,6 +236,10 @@ static int check_params(const vx_scene *s, const vx_frame_params *p, int w, int 
         if (p->cam_cell[i] <= -(1 << 22) || p->cam_cell[i] >= (1 << 22))
             return set_error(VX_EINVAL, "cam_cell out of range (|cell| < 2^22)");
     }
+    if (p->shadow_samples > VX_MAX_SHADOW_SAMPLES)
+        return set_error(VX_EINVAL, "shadow_samples must be <= VX_MAX_SHADOW_SAMPLES (16)");
+    if (p->shadow_samples > 1 && !(p->sun_radius >= 0.0f && p->sun_radius <= 0.5f))
+        return set_error(VX_EINVAL, "sun_radius must be in [0, 0.5] for soft shadows");
     return VX_OK;
 }
 
@@ -250,10 +254,16 @@ static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int 
     st->ao_samples = v[ST_AO];
     st->noise_px = v[ST_NOISE_PX];
     st->primary_cap_hits = v[ST_CAP_HITS];
-    // 4 B per field texel read, 32 B per trilinear AO, 80 B per
-    // clouded sky pixel (5 bilinear noise taps), plus the framebuffer store.
-    st->alg_bytes = 4ull * (st->primary_fetches + st->shadow_fetches) + 32ull * st->ao_samples +
-                    80ull * st->noise_px + (unsigned long long)out_bytes * st->pixels;
+    st->reflect_rays = v[ST_REFL_RAYS];
+    st->reflect_fetches = v[ST_REFL_FETCH];
+    st->rough_px = v[ST_ROUGH];
+    // 4 B per field texel read (primary, shadow and reflection
+    // rays), 32 B per trilinear AO, 80 B per clouded sky pixel (5 bilinear
+    // noise taps), 16 B per rough-normal white() tap (4 texels), plus the
+    // framebuffer store.
+    st->alg_bytes = 4ull * (st->primary_fetches + st->shadow_fetches + st->reflect_fetches) +
+                    32ull * st->ao_samples + 80ull * st->noise_px + 16ull * st->rough_px +
+                    (unsigned long long)out_bytes * st->pixels;
     st->kernel_ms = ms;
 }
 
@@ -278,6 +288,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
     a.Xp = s->L.Xp;
+    a.pad = s->L.pad;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
     a.XY = (unsigned)s->X * (unsigned)s->Y;
     a.XYZ = a.XY * (unsigned)s->Z;
@@ -489,6 +500,12 @@ void vx_sun_from_hour(double hour, float sun[3]) {   // map.js:399-402
     sun[0] = (float)(std::sin(hour) * std::sqrt(3.0 / 4.0));
     sun[1] = (float)(std::sin(hour) * std::sqrt(1.0 / 4.0));
     sun[2] = (float)std::fabs(std::cos(hour));
+}
+
+int vx_sun_samples(const float sun[3], float radius, int n, float out[][3]) {
+    if (!sun || !out) return set_error(VX_EINVAL, "vx_sun_samples: null argument");
+    sun_samples(sun, radius, n, out);
+    return VX_OK;
 }
 
 int vx_decode(const void *in, size_t n, int format, const char *key, void *out, size_t out_cap, size_t *out_size) {

@@ -5,6 +5,7 @@
 // on uniforms, so the host derives them once here with exactly the fp32
 // operations, operation order and IEEE rounding the oracle uses per pixel
 // (x86-64 SSE, -ffp-contract=off): the kernel then reads bit-identical values.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -15,6 +16,65 @@ namespace vx {
 static inline float gmax(float x, float y) { return x < y ? y : x; }
 static inline float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
 static inline float gsign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+
+void sun_ray(const float r[3], SunRay &s) {
+    for (int i = 0; i < 3; i++) {
+        s.r[i] = r[i];
+        s.sign[i] = gsign(r[i]);
+        s.abs[i] = std::fabs(r[i]);
+        s.rcp[i] = s.abs[i] != 0.0f ? 1.0f / s.abs[i] : 0.0f;
+    }
+    s.up = r[2] > 0.0f ? 1 : 0;
+    const float lim = 0.0009765625f;   // 2^-10: keeps every t = d/|r| < 1025, every cell index in int range
+    s.fast = s.abs[0] >= lim && s.abs[1] >= lim && s.abs[2] >= lim;
+}
+
+// cos/sin of k * golden angle (Vogel spiral), k = 0..15, as literals: no libm
+// trigonometry enters the directions, so host and oracle agree bit for bit.
+static const double kVogel[VX_MAX_SHADOW_SAMPLES][2] = {
+    {1.0, 0.0},
+    {-0.7373688780783197, 0.6754902942615238},
+    {0.08742572471695988, -0.9961710408648278},
+    {0.6084388609788626, 0.7936007512916959},
+    {-0.9847134853154287, -0.17418195037931164},
+    {0.8437552948123972, -0.5367280526263227},
+    {-0.25960430490148856, 0.9657150743757783},
+    {-0.4609070247133692, -0.8874484292452546},
+    {0.9393212963241181, 0.343038630874102},
+    {-0.9243455561378048, 0.38155640847493627},
+    {0.4238459950479107, -0.9057342725556136},
+    {0.2992838644448729, 0.954164120307897},
+    {-0.86521120975323, -0.5014075812324265},
+    {0.976675773628176, -0.21471942904125782},
+    {-0.5751294291397393, 0.8180624302199665},
+    {-0.12851068979899324, -0.9917081236973845},
+};
+
+// Soft-shadow sample k of n: the sun pushed by radius*sqrt((k+0.5)/n) along
+// spiral angle k in the plane normal to it (u = normalize(a x sun), v = sun x u,
+// a = z, or x when |sun.z| >= 0.9), normalised; double, then rounded to float.
+void sun_samples(const float sun[3], float radius, int n, float out[][3]) {
+    if (n <= 1) {
+        for (int i = 0; i < 3; i++) out[0][i] = sun[i];
+        return;
+    }
+    n = n > VX_MAX_SHADOW_SAMPLES ? VX_MAX_SHADOW_SAMPLES : n;
+    const double sd[3] = {sun[0], sun[1], sun[2]};
+    const bool zax = std::fabs(sd[2]) < 0.9;
+    const double ax[3] = {zax ? 0.0 : 1.0, 0.0, zax ? 1.0 : 0.0};
+    double u[3] = {ax[1] * sd[2] - ax[2] * sd[1], ax[2] * sd[0] - ax[0] * sd[2], ax[0] * sd[1] - ax[1] * sd[0]};
+    const double ul = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    for (double &c : u) c /= ul;
+    const double v[3] = {sd[1] * u[2] - sd[2] * u[1], sd[2] * u[0] - sd[0] * u[2], sd[0] * u[1] - sd[1] * u[0]};
+    for (int k = 0; k < n; k++) {
+        const double r = (double)radius * std::sqrt(((double)k + 0.5) / (double)n);
+        const double cu = r * kVogel[k][0], cv = r * kVogel[k][1];
+        double x[3];
+        for (int i = 0; i < 3; i++) x[i] = sd[i] + cu * u[i] + cv * v[i];
+        const double l = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+        for (int i = 0; i < 3; i++) out[k][i] = (float)(x[i] / l);
+    }
+}
 
 void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, int max_steps, FrameConsts &fc) {
     std::memset(&fc, 0, sizeof fc);
@@ -67,6 +127,10 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
     fc.skyOff[1] = 1e-4f * ((float)p.cam_cell[1] + p.cam_fract[1]);
     fc.quality = p.quality;
     fc.flags = p.flags;
+    fc.n_sun = p.shadow_samples > 1 ? std::min(p.shadow_samples, VX_MAX_SHADOW_SAMPLES) : 1;
+    float dirs[VX_MAX_SHADOW_SAMPLES][3];
+    sun_samples(p.sun_dir, p.sun_radius, fc.n_sun, dirs);
+    for (int k = 0; k < fc.n_sun; k++) sun_ray(dirs[k], fc.sun_k[k]);
 }
 
 }  // namespace vx

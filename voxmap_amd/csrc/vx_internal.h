@@ -11,6 +11,17 @@ namespace vx {
 // message in a thread-local buffer (vx_last_error).
 int set_error(int code, const std::string &msg);
 
+// One sun direction of the march (render.frag:75-142) with the per-frame
+// constants its loop needs: sign(r), |r|, RN(1/|r|) (Markstein division).
+struct SunRay {
+    float r[3], sign[3], abs[3], rcp[3];
+    int up;                            // r.z > 0: march reads R, else G (render.frag:89)
+    int fast;                          // every 2^-10 <= |r_i|: fast exact march path
+};
+void sun_ray(const float r[3], SunRay &s);
+// ext soft shadows: the sun-disc sample directions
+void sun_samples(const float sun[3], float radius, int n, float out[][3]);
+
 // Per-frame constants derived on the host from vx_frame_params with the same
 // fp32 operations (same order, IEEE, no contraction) the oracle performs per
 // pixel, so the kernel reads bit-identical values.
@@ -33,6 +44,8 @@ struct FrameConsts {
     float skyOff[2];                   // 1e-4 * (u_cellPos.xy + u_fractPos.xy) (render.frag:191)
     int quality;
     unsigned flags;
+    int n_sun;                         // ext: sun samples per shadow (1 = the reference's hard shadow)
+    SunRay sun_k[VX_MAX_SHADOW_SAMPLES];   // ext: soft-shadow sample directions
 };
 
 // Parameters of one render launch (passed by value to the kernel).
@@ -53,6 +66,7 @@ struct KernelArgs {
     vx_frame_params p;
     int max_shadow_steps;
     int Xp;                  // padded row length (FieldLayout)
+    int pad;                 // border width of the prim copies (FieldLayout::pad)
     unsigned XpYp;           // padded slice size
     unsigned XY, XYZ;        // X*Y, X*Y*Z
     unsigned copy_texels;    // cells per prim copy (FieldLayout::texels)
@@ -64,7 +78,7 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
 
 enum StatSlot {
     ST_PIXELS = 0, ST_SKY, ST_BLOCK, ST_GLASS, ST_PRIM_FETCH, ST_SHADOW_RAYS, ST_SHADOW_FETCH,
-    ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_COUNT
+    ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_REFL_RAYS, ST_REFL_FETCH, ST_ROUGH, ST_COUNT
 };
 
 // Field data in HBM (vx_kernels.hip): `prim` = 8 copies (one

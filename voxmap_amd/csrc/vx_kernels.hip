@@ -105,6 +105,7 @@ struct Surf {            // one G-buffer record (what render.vert hands render.f
 
 struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
+    unsigned refl_rays, refl_fetch, rough;   // extensions
 };
 
 // Field data in HBM, each array shaped for the loop that
@@ -127,8 +128,8 @@ __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y,
 
 // ---------------- sun march: render.frag:75-142 ----------------
 // Fast exact path for sun directions with every |r_i| >= 2^-10 (no zero
-// component, so no 0*inf NaN; every t finite and < 1025).  CH = channel read
-// by sdf_dir (0: R "up" for r.z > 0, 1: G "down").  Returns "lit"
+// component, so no 0*inf NaN; every t finite and < 1025).  `sun` is the
+// channel sdf_dir reads (R "up" for r.z > 0, else G "down").  Returns "lit"
 // (step == MAX_STEPS, render.frag:234).
 //
 // Loop shape: one exit test per step (sky, safe == 0 or the step budget),
@@ -136,14 +137,13 @@ __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y,
 // min3/med3 (two or more axes share the minimum iff med3 == min3, then the
 // literal length of render.frag:105-116), and a sky lane's load redirected to
 // cell 0 instead of branching around it.
-template <int CH>   // CH: documents the channel; the caller passes its array
-__device__ bool march_fast(const KernelArgs &a, const uint8_t *sun, int c0, int c1, int c2, float f0, float f1, float f2,
-                           unsigned &fetches) {
+__device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
+                           float f1, float f2, unsigned &fetches) {
     const FrameConsts &F = a.fc;
-    const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
-    const float b0 = F.sun_abs[0], b1 = F.sun_abs[1], b2 = F.sun_abs[2];
-    const float y0 = F.sun_rcp[0], y1 = F.sun_rcp[1], y2 = F.sun_rcp[2];
-    const float r0 = F.sun[0], r1 = F.sun[1], r2 = F.sun[2];
+    const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
+    const float b0 = S.abs[0], b1 = S.abs[1], b2 = S.abs[2];
+    const float y0 = S.rcp[0], y1 = S.rcp[1], y2 = S.rcp[2];
+    const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
     if (maxs <= 0) return maxs == 0;
     float safe = 1.0f;
@@ -182,13 +182,12 @@ __device__ bool march_fast(const KernelArgs &a, const uint8_t *sun, int c0, int 
 
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
-__device__ bool march_literal(const KernelArgs &a, const uint8_t *sun, int c0, int c1, int c2, float f0, float f1, float f2,
-                              unsigned &fetches) {
+__device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
+                              float f1, float f2, unsigned &fetches) {
     const FrameConsts &F = a.fc;
-    const float s0 = F.sun_sign[0], s1 = F.sun_sign[1], s2 = F.sun_sign[2];
-    const float a0 = F.sun_abs[0], a1 = F.sun_abs[1], a2 = F.sun_abs[2];
-    const float r0 = F.sun[0], r1 = F.sun[1], r2 = F.sun[2];
-    const int sh = F.sun_up ? 0 : 8;
+    const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
+    const float a0 = S.abs[0], a1 = S.abs[1], a2 = S.abs[2];
+    const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
     float safe = 1.0f;
     int step = 0;
@@ -216,6 +215,14 @@ __device__ bool march_literal(const KernelArgs &a, const uint8_t *sun, int c0, i
         step++;
     }
     return step == maxs;
+}
+
+// march(cell, fract, S.r) of render.frag:233 -> "lit" (step == MAX_STEPS, :234)
+__device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay &S, int c0, int c1, int c2, float f0,
+                                          float f1, float f2, unsigned &fetches) {
+    const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
+    return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, fetches)
+                  : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, fetches);
 }
 
 // ---------------- primary visibility ----------------
@@ -492,17 +499,65 @@ __device__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, flo
     o[0] = sky[0]; o[1] = sky[1]; o[2] = sky[2]; o[3] = 1.0f;
 }
 
+// ---------------- extensions (DESIGN.md §3 "Extensions") ----------------
+// white(p) = 1 - 2*texture(u_noise, p).rgb (render.frag:16-21), bilinear REPEAT LOD 0.
+__device__ void white(const KernelArgs &a, const float *unorm, float px, float py, float &w0, float &w1, float &w2) {
+    const int W = a.noise_w, H = a.noise_h;
+    const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
+    const float fu = floorf(u), fv = floorf(v);
+    const float wa = u - fu, wb = v - fv;
+    const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
+    const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+    const uint32_t t00 = a.noise[(unsigned)y0 * W + x0], t10 = a.noise[(unsigned)y0 * W + x1];
+    const uint32_t t01 = a.noise[(unsigned)y1 * W + x0], t11 = a.noise[(unsigned)y1 * W + x1];
+    float w[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const int sh = 8 * ch;
+        const float r0 = gmix(unorm[(t00 >> sh) & 0xff], unorm[(t10 >> sh) & 0xff], wa);
+        const float r1 = gmix(unorm[(t01 >> sh) & 0xff], unorm[(t11 >> sh) & 0xff], wa);
+        w[ch] = 1.0f - 2.0f * gmix(r0, r1, wb);
+    }
+    w0 = w[0]; w1 = w[1]; w2 = w[2];
+}
+
+constexpr float kRoughScale = 0.00390625f;   // 1/256: 4 noise texels per voxel
+constexpr float kRoughAmp = 0.1f;
+
 // ---------------- render.frag main(), block branch (render.frag:148-176, 207-251) ----------------
-__device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt) {
+// EXT: the extension instantiation (rough normals, soft shadows); has_ray:
+// rayDir is given (a surface seen in a reflection) instead of the camera ray
+// to the fragment (:154).  ray_out receives the rayDir used.
+template <bool EXT>
+__device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt,
+                            bool has_ray = false, float q0 = 0.0f, float q1 = 0.0f, float q2 = 0.0f,
+                            float *ray_out = nullptr) {
     const FrameConsts &F = a.fc;
     const int ni = g.nidx;
     const float n0 = ni == 0 ? 1.0f : (ni == 1 ? -1.0f : 0.0f);
     const float n1 = ni == 2 ? 1.0f : (ni == 3 ? -1.0f : 0.0f);
     const float n2 = ni == 4 ? 1.0f : (ni == 5 ? -1.0f : 0.0f);
     float r0, r1, r2;
-    normalize3((float)(g.c0 - F.cam_cell[0]) + (g.f0 - F.cam_fract[0]),
-               (float)(g.c1 - F.cam_cell[1]) + (g.f1 - F.cam_fract[1]),
-               (float)(g.c2 - F.cam_cell[2]) + (g.f2 - F.cam_fract[2]), r0, r1, r2);   // :154
+    if (EXT && has_ray) {
+        r0 = q0; r1 = q1; r2 = q2;
+    } else {
+        normalize3((float)(g.c0 - F.cam_cell[0]) + (g.f0 - F.cam_fract[0]),
+                   (float)(g.c1 - F.cam_cell[1]) + (g.f1 - F.cam_fract[1]),
+                   (float)(g.c2 - F.cam_cell[2]) + (g.f2 - F.cam_fract[2]), r0, r1, r2);   // :154
+    }
+    if (EXT && ray_out) { ray_out[0] = r0; ray_out[1] = r1; ray_out[2] = r2; }
+    // shading normal: geometric, or (ext ROUGH) jittered by white() noise
+    float m0 = n0, m1 = n1, m2 = n2;
+    const bool rough = EXT && (F.flags & VX_FLAG_ROUGH);
+    if (rough) {
+        cnt.rough++;
+        const int ax = ni >> 1;
+        const float u = ax == 0 ? (float)g.c1 + g.f1 : (float)g.c0 + g.f0;   // first in-face axis
+        const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;   // second
+        float w0, w1, w2;
+        white(a, unorm, u * kRoughScale, v * kRoughScale, w0, w1, w2);
+        normalize3(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+    }
     float base0 = 1.0f, base1 = 1.0f, base2 = 1.0f;
     if (g.color < 22) { base0 = kPalette[g.color][0]; base1 = kPalette[g.color][1]; base2 = kPalette[g.color][2]; }
     float amb0 = 1.0f, amb1 = 1.0f, amb2 = 1.0f;
@@ -515,35 +570,140 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
         amb2 = gmix(1.0f, F.shadeCol[2], ambFactor);
     }
     float shadeFactor = F.shadeFactor[ni];                                             // :228-229
+    if (rough)
+        shadeFactor = F.sun[2] < 0.0f ? 0.0f : sqrtf(gmax(0.0f, (m0 * F.sun[0] + m1 * F.sun[1]) + m2 * F.sun[2]));
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
-        cnt.shadow_rays++;
-        bool lit;
-        if (F.march_fast)
-            lit = F.sun_up ? march_fast<0>(a, a.sun, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch)
-                           : march_fast<1>(a, a.sun + a.XYZ, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
-        else
-            lit = march_literal(a, F.sun_up ? a.sun : a.sun + a.XYZ, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
-        shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
+        if (!EXT || F.n_sun <= 1) {
+            cnt.shadow_rays++;
+            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+            shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
+        } else {                       // ext soft shadows: lit fraction of the sun samples
+            int lit = 0;
+            for (int k = 0; k < F.n_sun; k++) {
+                cnt.shadow_rays++;
+                lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch) ? 1 : 0;
+            }
+            shadeFactor = shadeFactor * ((float)lit / (float)F.n_sun);
+        }
     }
     const float l0 = F.shadeCol[0] + 0.4f * shadeFactor;                               // :238
     const float l1 = F.shadeCol[1] + 0.35f * shadeFactor;
     const float l2 = F.shadeCol[2] + 0.3f * shadeFactor;
     o[0] = base0; o[1] = base1; o[2] = base2; o[3] = 1.0f;
     if (F.quality > 0) {                                                               // :242-244
-        o[0] = o[0] * ((F.normalCol[ni][0] * l0) * amb0);
-        o[1] = o[1] * ((F.normalCol[ni][1] * l1) * amb1);
-        o[2] = o[2] * ((F.normalCol[ni][2] * l2) * amb2);
+        float nc0 = F.normalCol[ni][0], nc1 = F.normalCol[ni][1], nc2 = F.normalCol[ni][2];
+        if (rough) {                                                                   // :211-217 per fragment
+            const float an0 = fabsf(m0), an1 = fabsf(m1), an2 = fabsf(m2);
+            nc0 = (0.90f * an0 + 0.95f * an1) + 1.0f * an2;
+            nc1 = (0.90f * an0 + 0.95f * an1) + 1.0f * an2;
+            nc2 = (0.95f * an0 + 1.00f * an1) + 1.0f * an2;
+            if (m2 < 0.0f) { nc0 = nc0 * 0.8f; nc1 = nc1 * 0.8f; nc2 = nc2 * 0.8f; }
+        }
+        o[0] = o[0] * ((nc0 * l0) * amb0);
+        o[1] = o[1] * ((nc1 * l1) * amb1);
+        o[2] = o[2] * ((nc2 * l2) * amb2);
     }
     if (g.id == 2) {                                                                   // :246-249
-        const float k = 2.0f * ((n0 * r0 + n1 * r1) + n2 * r2);
-        const float rz = sqrtf(gmax(0.0f, r2 - k * n2));
-        o[3] = 0.8f * vexp2((r0 * n0 + r1 * n1) + r2 * n2);
+        const float k = 2.0f * ((m0 * r0 + m1 * r1) + m2 * r2);
+        const float rz = sqrtf(gmax(0.0f, r2 - k * m2));
+        o[3] = 0.8f * vexp2((r0 * m0 + r1 * m1) + r2 * m2);
 #pragma unroll
         for (int i = 0; i < 3; i++) {
             const float atm = gmix(F.scatterCol[i], F.spaceCol[i], rz);
             o[i] = o[i] * (0.2f * atm);
         }
     }
+}
+
+// ext REFLECT: octant-cube walk of a reflection ray B + o + t*d (B integer,
+// 0 <= o < 1, start cell B + c) to the first colour change (oracle walk()
+// with glass_layer = 0).  Scalar form of primary(): reflection rays are few.
+// Returns 1 and the surface record, or 0 (sky: left the grid, or the start
+// cell is outside it).
+__device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o0, float o1, float o2, float d0,
+                            float d1, float d2, int c0, int c1, int c2, Surf &h, Counters &cnt) {
+    const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
+    const uint16_t *pp = a.prim + (size_t)oct * a.copy_texels;
+    auto inside = [&](int x, int y, int z) {
+        return (unsigned)x < (unsigned)a.X && (unsigned)y < (unsigned)a.Y && (unsigned)z < (unsigned)a.Z;
+    };
+    auto fetch = [&](int x, int y, int z) -> uint32_t {
+        return pp[(unsigned)(x + a.pad) + (unsigned)a.Xp * (unsigned)(y + a.pad) + a.XpYp * (unsigned)(z + a.pad)];
+    };
+    const int st0 = d0 > 0.0f ? 1 : -1, st1 = d1 > 0.0f ? 1 : -1, st2 = d2 > 0.0f ? 1 : -1;
+    const float iv0 = d0 != 0.0f ? 1.0f / d0 : 0.0f, iv1 = d1 != 0.0f ? 1.0f / d1 : 0.0f,
+                iv2 = d2 != 0.0f ? 1.0f / d2 : 0.0f;
+    int x = B0 + c0, y = B1 + c1, z = B2 + c2;
+    if (!inside(x, y, z)) return 0;
+    uint32_t t = fetch(x, y, z);
+    cnt.refl_fetch++;
+    int prev = t & 0xff, R = (int)(t >> 8);
+    const int cap = 4 * (a.X + a.Y + a.Z);
+    for (int it = 0; it < cap; it++) {
+        const float tb0 = d0 != 0.0f ? ((float)(c0 + (st0 > 0 ? R + 1 : -R)) - o0) * iv0 : kInf;
+        const float tb1 = d1 != 0.0f ? ((float)(c1 + (st1 > 0 ? R + 1 : -R)) - o1) * iv1 : kInf;
+        const float tb2 = d2 != 0.0f ? ((float)(c2 + (st2 > 0 ? R + 1 : -R)) - o2) * iv2 : kInf;
+        const int ax = (tb0 <= tb1 && tb0 <= tb2) ? 0 : (tb1 <= tb2 ? 1 : 2);
+        const float te = ax == 0 ? tb0 : (ax == 1 ? tb1 : tb2);
+        auto side = [&](int c, float o, float d) {
+            const int v = f2i(floorf(o + te * d));
+            const int lo = d < 0.0f ? c - R : c, hi = d < 0.0f ? c : c + R;
+            return v < lo ? lo : (v > hi ? hi : v);
+        };
+        const int n0 = ax == 0 ? c0 + st0 * (R + 1) : side(c0, o0, d0);
+        const int n1 = ax == 1 ? c1 + st1 * (R + 1) : side(c1, o1, d1);
+        const int n2 = ax == 2 ? c2 + st2 * (R + 1) : side(c2, o2, d2);
+        c0 = n0; c1 = n1; c2 = n2;
+        x = B0 + c0; y = B1 + c1; z = B2 + c2;
+        if (!inside(x, y, z)) return 0;
+        t = fetch(x, y, z);
+        cnt.refl_fetch++;
+        const int col = t & 0xff;
+        R = (int)(t >> 8);
+        if (col != prev) {
+            const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
+            h.color = col;
+            h.id = col == kGlass ? 2 : 0;
+            h.nidx = 2 * ax + (stp > 0 ? 1 : 0);
+            h.c0 = x + (ax == 0 && stp < 0 ? 1 : 0);
+            h.c1 = y + (ax == 1 && stp < 0 ? 1 : 0);
+            h.c2 = z + (ax == 2 && stp < 0 ? 1 : 0);
+            h.f0 = ax == 0 ? 0.0f : (o0 + te * d0) - (float)c0;
+            h.f1 = ax == 1 ? 0.0f : (o1 + te * d1) - (float)c1;
+            h.f2 = ax == 2 ? 0.0f : (o2 + te * d2) - (float)c2;
+            return 1;
+        }
+        prev = col;
+    }
+    cnt.cap_hit++;
+    return 0;
+}
+
+// ext REFLECT: colour seen along the mirror reflection at glass record gl
+// (rd = the camera rayDir at the fragment; R = rd with the face-axis
+// component negated = reflect(rd, n) exactly), oracle reflect_color().
+__device__ void reflect_color(const KernelArgs &a, const float *unorm, const Surf &gl, const float rd[3], float out[3],
+                              Counters &cnt) {
+    const int ax = gl.nidx >> 1;
+    const float R0 = ax == 0 ? -rd[0] : rd[0], R1 = ax == 1 ? -rd[1] : rd[1], R2 = ax == 2 ? -rd[2] : rd[2];
+    const float fl0 = floorf(gl.f0), fl1 = floorf(gl.f1), fl2 = floorf(gl.f2);
+    const int B0 = ax == 0 ? gl.c0 : gl.c0 + f2i(fl0);
+    const int B1 = ax == 1 ? gl.c1 : gl.c1 + f2i(fl1);
+    const int B2 = ax == 2 ? gl.c2 : gl.c2 + f2i(fl2);
+    const float o0 = ax == 0 ? 0.0f : gl.f0 - fl0;
+    const float o1 = ax == 1 ? 0.0f : gl.f1 - fl1;
+    const float o2 = ax == 2 ? 0.0f : gl.f2 - fl2;
+    const int s0 = ax == 0 ? (R0 > 0.0f ? 0 : -1) : 0;
+    const int s1 = ax == 1 ? (R1 > 0.0f ? 0 : -1) : 0;
+    const int s2 = ax == 2 ? (R2 > 0.0f ? 0 : -1) : 0;
+    cnt.refl_rays++;
+    Surf h;
+    float rgba[4];
+    if (walk_reflect(a, B0, B1, B2, o0, o1, o2, R0, R1, R2, s0, s1, s2, h, cnt))
+        shade_block<true>(a, unorm, h, rgba, cnt, true, R0, R1, R2);
+    else
+        shade_sky(a, unorm, R0, R1, R2, rgba, cnt);
+    out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
 }
 
 // =====================================================================
@@ -591,7 +751,9 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
 }
 
 // Lane = pixel, wave = 8x8 tile, workgroup = 16x16 pixels.
-template <int FMT, bool STATS, bool TILED>
+// EXT: the extension instantiation (REFLECT, ROUGH, soft shadows); the v1
+// instantiation does not carry their registers or code.
+template <int FMT, bool STATS, bool TILED, bool EXT>
 __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
     // unorm8 -> float table: b/255 as IEEE quotients (render.frag:38 decode)
     __shared__ float s_unorm[256];
@@ -616,7 +778,7 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
     }
     const int px = ox + lx, py = oy + ly;
     const FrameConsts &F = a.fc;
-    Counters cnt = {0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
     if (px < a.w && py < a.h) {
         float d0, d1, d2;
@@ -635,11 +797,23 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
             n_sky = 1;
             shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
-            shade_block(a, s_unorm, g[0], rgba, cnt);
+            float rd[3];
+            shade_block<EXT>(a, s_unorm, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd);
             if (g[0].id == 2) {
                 n_glass = 1;
+                if (EXT && (F.flags & VX_FLAG_REFLECT)) {
+                    // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
+                    float refl[3];
+                    reflect_color(a, s_unorm, g[0], rd, refl, cnt);
+                    const int ax = g[0].nidx >> 1;
+                    const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
+                    const float x = 1.0f - cs, x2 = x * x;
+                    const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
+                }
                 float dst[4];
-                if (n == 2) shade_block(a, s_unorm, g[1], dst, cnt);
+                if (n == 2) shade_block<EXT>(a, s_unorm, g[1], dst, cnt);
                 else shade_sky(a, s_unorm, d0, d1, d2, dst, cnt);
                 const float al = rgba[3];
 #pragma unroll
@@ -667,6 +841,9 @@ __global__ __launch_bounds__(256) void k_render(KernelArgs a) {
         v[ST_AO] = wave_sum(cnt.ao);
         v[ST_NOISE_PX] = wave_sum(cnt.noise_px);
         v[ST_CAP_HITS] = wave_sum(cnt.cap_hit);
+        v[ST_REFL_RAYS] = wave_sum(cnt.refl_rays);
+        v[ST_REFL_FETCH] = wave_sum(cnt.refl_fetch);
+        v[ST_ROUGH] = wave_sum(cnt.rough);
         if (lane == 0) {
             // spread the adds over 64 slot rows to avoid one hot line per counter
             unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
@@ -741,11 +918,14 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
     const bool st = a.stats != nullptr;
     dim3 block(256);
     dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_size >> 4) * (a.tile_size >> 4)) : dim3((a.w + 15) / 16, (a.h + 15) / 16);
-#define VX_L(F, S, T) hipLaunchKernelGGL((k_render<F, S, T>), grid, block, 0, s, a)
-#define VX_LT(F, S) do { if (tiled) VX_L(F, S, true); else VX_L(F, S, false); } while (0)
+    const bool ext = (a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) || a.fc.n_sun > 1;
+#define VX_L(F, S, T, E) hipLaunchKernelGGL((k_render<F, S, T, E>), grid, block, 0, s, a)
+#define VX_LE(F, S, T) do { if (ext) VX_L(F, S, T, true); else VX_L(F, S, T, false); } while (0)
+#define VX_LT(F, S) do { if (tiled) VX_LE(F, S, true); else VX_LE(F, S, false); } while (0)
     if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_LT(0, true); else VX_LT(0, false); }
     else { if (st) VX_LT(1, true); else VX_LT(1, false); }
 #undef VX_LT
+#undef VX_LE
 #undef VX_L
     if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
     return (int)hipGetLastError();

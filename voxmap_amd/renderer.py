@@ -66,7 +66,7 @@ class Frame:
 
 
 def make_frame(sbj, rot, w, h, *, sun=None, hour=1.0, time=123.0, quality=1, frame=0,
-               flags=0, max_shadow_steps=0) -> Frame:
+               flags=0, max_shadow_steps=0, shadow_samples=0, sun_radius=0.0) -> Frame:
     p = frame_from_orbit(sbj, rot, w, h)
     sd = sun if sun is not None else sun_from_hour(hour)
     for i in range(3):
@@ -76,7 +76,19 @@ def make_frame(sbj, rot, w, h, *, sun=None, hour=1.0, time=123.0, quality=1, fra
     p.frame = int(frame)
     p.flags = int(flags)
     p.max_shadow_steps = int(max_shadow_steps)
+    p.shadow_samples = int(shadow_samples)  # ext soft shadows (<= 1: hard, render.frag:232-235)
+    p.sun_radius = float(sun_radius)
     return Frame(p, int(w), int(h))
+
+
+def sun_samples(sun, radius: float, n: int):
+    """The soft-shadow sun directions a frame with ``shadow_samples = n`` marches (vx_sun_samples)."""
+    import numpy as _np
+    m = max(1, min(int(n), _abi.MAX_SHADOW_SAMPLES))
+    out = _np.zeros((m, 3), _np.float32)
+    check(lib().vx_sun_samples((C.c_float * 3)(*sun), float(radius), int(n),
+                               out.ctypes.data_as(C.POINTER(C.c_float))))
+    return out
 
 
 class Scene:
@@ -243,4 +255,5 @@ def params_to_dict(p: FrameParams) -> dict:
         "cam_cell": list(p.cam_cell), "cam_fract": _f3(p.cam_fract), "sun_dir": _f3(p.sun_dir),
         "ray_fwd": _f3(p.ray_fwd), "ray_right": _f3(p.ray_right), "ray_up": _f3(p.ray_up),
         "flags": p.flags, "max_shadow_steps": p.max_shadow_steps,
+        "shadow_samples": p.shadow_samples, "sun_radius": p.sun_radius,
     }
