@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark of the Voxmap shading path on MI355X (BASELINE.json metric).
 
-A step renders one full frame of the headline workload (C3: 3840x2160, the
-reference's v1 shading = primary visibility + sun march + AO + sky/clouds +
-glass, on the synthetic S-proc 1024x256x32 field, camera K1) from the
-HBM-resident field into an HBM-resident RGBA8 framebuffer.
+A step renders one full frame of the headline workload (BASELINE configs[2],
+C3: 3840x2160 "full quality" = the reference's v1 shading (primary visibility +
+sun march + AO + sky/clouds + glass) + the f-3 extensions reflection and rough
+normals, on the synthetic S-proc 1024x256x32 field, camera K1) from the
+HBM-resident field into an HBM-resident RGBA8 framebuffer.  The v1 shading
+alone (the reference's own shader, flags 0) is timed in the same run and
+reported under config.v1.  --config C5: the 3^3-upscaled 3072x768x96 field
+with 16-sample soft shadows (BASELINE configs[4]).
 
 N > 1 GPUs (one process per GPU, torchrun): weak scaling — the frame grows
 with N (W = 3840*sqrt(N), H = 2160*sqrt(N), so N = 4 is C4's 7680x4320),
@@ -39,8 +43,12 @@ def parse():
     ap.add_argument("--camera", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--flags", type=int, default=0, help="VX_FLAG_* ablation bits (diagnostics; 0 = headline)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+    ap.add_argument("--quality", choices=["full", "v1"], default="full",
+                    help="full = v1 + REFLECT + ROUGH (BASELINE 'full quality'); v1 = the reference shader only")
+    ap.add_argument("--flags", type=int, default=None, help="VX_FLAG_* bits overriding --quality (diagnostics)")
+    ap.add_argument("--samples", type=int, default=None, help="soft-shadow samples (default: 16 for C5, else 1)")
+    ap.add_argument("--sun-radius", type=float, default=0.03)
+    ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes measured by rocprofv3 PMC (tools/pmc_traffic.py)")
     return ap.parse_args()
 
@@ -78,7 +86,10 @@ def main():
     noise = vx.noise_synth(0)
     scene = vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
                      noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=local)
-    frame = presets.camera_frame(cam, W, H, scale=up, flags=args.flags)
+    flags = args.flags if args.flags is not None else (vx.FLAG_FULL_QUALITY if args.quality == "full" else 0)
+    samples = args.samples if args.samples is not None else cfg.get("samples", 1)
+    frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
+                                 sun_radius=args.sun_radius if samples > 1 else 0.0)
     torch_stream = torch.cuda.Stream()          # a real stream: torch events and the kernels share it
     torch.cuda.set_stream(torch_stream)
     stream = torch_stream.cuda_stream
@@ -137,7 +148,28 @@ def main():
         t_local = float(tt.item())
     ms_per_step = 1000.0 * t_local / args.steps
 
-    rays = stats["pixels"] + stats["shadow_rays"]              # rays actually marched per frame
+    v1 = None
+    if world == 1 and flags != 0 and args.flags is None and samples <= 1:
+        # the reference's own shader (v1, flags 0) on the same frame, same stream
+        fr1 = presets.camera_frame(cam, W, H, scale=up)
+        st1 = scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
+        for _ in range(args.warmup):
+            scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+        e1.record()
+        torch.cuda.synchronize()
+        ms1 = e0.elapsed_time(e1) / args.steps
+        r1 = st1.pixels + st1.shadow_rays
+        v1 = {"ms_per_frame": round(ms1, 4), "mrays_per_s": round(r1 / ms1 / 1e3, 3), "rays_per_frame": int(r1),
+              "alg_bytes": int(st1.alg_bytes), "roofline_frac": round(st1.alg_bytes / (ms1 * 1e-3) / 1e9 /
+                                                                      HBM_PEAK_GBPS, 4)}
+
+    rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
     value = rays * args.steps / t_local / 1e6                 # whole-job Mrays/s
     result = None
     if rank == 0:
@@ -145,15 +177,19 @@ def main():
         kernel_ms = ev_ms if world == 1 else stats["kernel_ms"]
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = None
-        if world == 1 and os.path.exists(args.traffic_json):
+        tj_path = args.traffic_json or os.path.join(
+            ROOT, "profiles", "traffic_r01.json" if args.config != "C5" else "traffic_r01_c5.json")
+        if world == 1 and os.path.exists(tj_path):
             try:
-                tj = json.load(open(args.traffic_json))
-                if tj.get("config") == args.config and tj.get("camera") == cam:
+                tj = json.load(open(tj_path))
+                if (tj.get("config") == args.config and tj.get("camera") == cam and tj.get("flags", 0) == flags
+                        and tj.get("samples", 1) == samples):
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         result = {
-            "metric": f"Mrays/s at {cfg['w']}x{cfg['h']} full quality ({args.config}); fps; % HBM roofline",
+            "metric": f"Mrays/s at {cfg['w']}x{cfg['h']} {'full quality' if flags else 'v1 shading'} "
+                      f"({args.config}); fps; % HBM roofline",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -164,22 +200,28 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic S-proc field (seed 1) in map.bin layout; synthetic noise texture (real map.blob is "
-                    "AES-encrypted, key not in repo)",
+            "data": f"synthetic {cfg['scene']} field (seed 1) in map.bin layout; synthetic noise texture (real "
+                    "map.blob is AES-encrypted, key not in repo)",
             "config": {
-                "workload": f"{args.config}: {W}x{H} frame, reference v1 shading (primary visibility + sun march + "
-                            f"trilinear AO + sky/clouds + glass), field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, "
-                            "RGBA8 framebuffer in HBM",
+                "workload": f"{args.config}: {W}x{H} frame, " + (
+                    "full quality = v1 shading (primary visibility + sun march + trilinear AO + sky/clouds + glass) "
+                    "+ ext reflection + rough normals" if flags == vx.FLAG_FULL_QUALITY else
+                    f"v1 shading flags={flags}") +
+                    (f" + {samples}-sample soft shadows (sun radius {args.sun_radius})" if samples > 1 else "") +
+                    f", field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, RGBA8 framebuffer in HBM",
+                "flags": flags, "shadow_samples": samples,
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
                 "tiles": {"size": TILE, "count": n_tiles, "assignment": "round-robin"} if world > 1 else None,
                 "fps": round(1000.0 / ms_per_step, 2),
                 "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
-                "shadow_rays": int(stats["shadow_rays"]),
+                "shadow_rays": int(stats["shadow_rays"]), "reflect_rays": int(stats["reflect_rays"]),
                 "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / t_local / 1e6, 3),
+                "v1": v1,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_render (fused primary+shade+shadow march)",
+                "kernel": "k_render (fused primary visibility + shading + sun march" +
+                          (" + reflection walk" if flags & vx.FLAG_REFLECT else "") + ")",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
@@ -223,15 +265,15 @@ def cpu_baseline(field, scene, noise, frame, W, H, target_s):
             t0 = time.perf_counter()
             _, st = o.render(frame.params, W, H, threads=threads, out=out)
             dt = time.perf_counter() - t0
-            rates.append((st.pixels + st.shadow_rays) / dt / 1e6)
-        desc = (f"{reps} full {W}x{H} frames ({st.pixels} pixels, {st.pixels + st.shadow_rays} rays each), "
-                f"median rate")
+            rates.append((st.pixels + st.shadow_rays + st.reflect_rays) / dt / 1e6)
+        desc = (f"{reps} full {W}x{H} frames ({st.pixels} pixels, {st.pixels + st.shadow_rays + st.reflect_rays} "
+                f"rays each), median rate")
     else:
         k = max(1, int(math.ceil(est_full / target_s)))
         t0 = time.perf_counter()
         _, st = o.render(frame.params, W, H, row0=k // 2, row_step=k, threads=threads, out=out)
         dt = time.perf_counter() - t0
-        rates.append((st.pixels + st.shadow_rays) / dt / 1e6)
+        rates.append((st.pixels + st.shadow_rays + st.reflect_rays) / dt / 1e6)
         desc = f"rows {k // 2}::{k} of the same {W}x{H} frame ({st.pixels} pixels) in {dt:.2f} s"
     return {
         "value": round(float(np.median(rates)), 4),

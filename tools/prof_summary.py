@@ -20,7 +20,10 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 src = sys.argv[2] if len(sys.argv) > 2 else f"gpurun_out/prof_{tag}"
 cfg = sys.argv[3] if len(sys.argv) > 3 else "C3"
 cam = sys.argv[4] if len(sys.argv) > 4 else "K1"
-KERNEL = "k_render<1, false, false>"
+flags = int(sys.argv[5]) if len(sys.argv) > 5 else 48          # VX_FLAG_FULL_QUALITY
+samples = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+# the bench's timed kernel: RGBA8, no stats, untiled; EXT instantiation unless v1
+KERNEL = f"k_render<1, false, false, {'true' if (flags & 0x30) or samples > 1 else 'false'}>"
 os.makedirs("profiles", exist_ok=True)
 shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"profiles/{tag}_kernel_stats.csv")
 
@@ -47,6 +50,7 @@ corr = (2 * fk + wk) * 1024
 pmc = {"kernel": KERNEL, "launches": [len(fetch), len(write)], "FETCH_SIZE_KiB_median": fk,
        "WRITE_SIZE_KiB_median": wk, "hbm_bytes_raw": raw, "hbm_bytes_read_x2": corr, "avg_duration_ns": avg_ns}
 json.dump(pmc, open(f"profiles/{tag}_pmc.json", "w"), indent=1)
-json.dump({"config": cfg, "camera": cam, "hbm_bytes_per_launch": int(corr), "hbm_bytes_raw": int(raw),
+json.dump({"config": cfg, "camera": cam, "flags": flags, "samples": samples,
+           "hbm_bytes_per_launch": int(corr), "hbm_bytes_raw": int(raw),
            "source": f"profiles/{tag}_pmc.json"}, open(f"profiles/traffic_{tag}.json", "w"), indent=1)
 print(json.dumps(pmc, indent=1))

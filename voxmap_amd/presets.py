@@ -27,7 +27,8 @@ CONFIGS = {
     "C2": {"w": 1920, "h": 1080, "scene": "s_proc", "camera": "K1", "note": "primary + shadow, 1 GPU"},
     "C3": {"w": 3840, "h": 2160, "scene": "s_proc", "camera": "K1", "note": "full v1 shading, 1 GPU"},
     "C4": {"w": 7680, "h": 4320, "scene": "s_proc", "camera": "K1", "note": "tiled across GPUs + RCCL gather"},
-    "C5": {"w": 3840, "h": 2160, "scene": "s_up3", "camera": "K1", "note": "3^3-upscaled field"},
+    "C5": {"w": 3840, "h": 2160, "scene": "s_up3", "camera": "K1", "samples": 16,
+           "note": "3^3-upscaled field, 16-sample soft shadows"},
 }
 
 
