@@ -72,6 +72,8 @@ def lib():
         L.vxo_pixel_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
         L.vxo_sun_samples.argtypes = [C.POINTER(C.c_float), C.c_float, C.c_int, C.POINTER(C.c_float)]
         L.vxo_sun_samples.restype = None
+        L.vxo_palette.argtypes = [C.POINTER(C.c_float)]
+        L.vxo_palette.restype = None
         L.vxo_exp2.argtypes = [C.c_float]
         L.vxo_exp2.restype = C.c_float
         L.vxo_field_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -150,6 +152,13 @@ def sun_samples(sun, radius: float, n: int) -> np.ndarray:
     out = np.zeros((m, 3), np.float32)
     lib().vxo_sun_samples((C.c_float * 3)(*sun), float(radius), int(n),
                           out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out
+
+
+def vxo_palette() -> np.ndarray:
+    """(22, 3) float32 palette of render.vert:21."""
+    out = np.zeros((22, 3), np.float32)
+    lib().vxo_palette(out.ctypes.data_as(C.POINTER(C.c_float)))
     return out
 
 

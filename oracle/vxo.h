@@ -119,6 +119,9 @@ void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3])
  * float).  n <= 1 gives the sun itself. */
 void vxo_sun_samples(const float sun[3], float radius, int n, float out[][3]);
 
+/* render.vert:21 palette(p) for p = 0..21. */
+void vxo_palette(float out[22][3]);
+
 /* Deterministic transcendental used by both oracle and kernel. */
 float vxo_exp2(float x);
 

@@ -93,6 +93,9 @@ static void palette(int p, float out[3]) {
     if (p >= 0 && p < 22) { out[0] = PALETTE[p][0]; out[1] = PALETTE[p][1]; out[2] = PALETTE[p][2]; }
     else { out[0] = out[1] = out[2] = 1.0f; } /* render.vert:21 trailing vec3(1) */
 }
+void vxo_palette(float out[22][3]) {
+    for (int p = 0; p < 22; p++) palette(p, out[p]);
+}
 static void normal_vec(int n, float out[3]) {
     out[0] = out[1] = out[2] = 0.0f;
     if (n >= 0 && n < 6) out[n >> 1] = (n & 1) ? -1.0f : 1.0f;

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for spec in "$@"; do
   label=${spec%%:*}; envs=${spec#*:}
   for f in ${AB_FLAGS:-0 8}; do
-    env ${envs//,/ } timeout -k 10 120 python bench.py --no-cpu --steps 30 --warmup 3 --flags $f > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 1; }
+    env ${envs//,/ } timeout -k 10 120 python bench.py --no-cpu --steps 30 --warmup 3 --flags $f ${AB_ARGS} > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 1; }
     echo "$label flags=$f $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab.log)"
   done
 done

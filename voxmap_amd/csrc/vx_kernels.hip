@@ -126,42 +126,49 @@ __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y,
     return (unsigned)x + __umul24((unsigned)a.X, (unsigned)y) + __umul24(a.XY, (unsigned)z);
 }
 
+// Buffer resource over a field array: loads take a 32-bit byte offset (no
+// 64-bit address arithmetic) and an offset past `bytes` reads 0 instead of
+// faulting.  Word 3 = 0x00020000: raw, untyped (gfx9 family).
 // ---------------- sun march: render.frag:75-142 ----------------
 // Fast exact path for sun directions with every |r_i| >= 2^-10 (no zero
 // component, so no 0*inf NaN; every t finite and < 1025).  `sun` is the
 // channel sdf_dir reads (R "up" for r.z > 0, else G "down").  Returns "lit"
 // (step == MAX_STEPS, render.frag:234).
 //
-// Loop shape: one exit test per step (sky, safe == 0 or the step budget),
-// cells kept as exact fp32 integers, the three-way min and its tie test as
-// min3/med3 (two or more axes share the minimum iff med3 == min3, then the
-// literal length of render.frag:105-116), and a sky lane's load redirected to
-// cell 0 instead of branching around it.
+// Loop shape: rotated so that the step length of the NEXT step (fract,
+// three divisions, min3: it depends only on f) is computed while the texel
+// load of this step is in flight; the dependent chain of a step is then just
+// safe -> f -> floor -> cell -> address -> load.  One exit test per step
+// (sky, safe == 0 or the step budget); cells kept as exact fp32 integers; the
+// three-way min and its tie test as min3/med3 (two or more axes share the
+// minimum iff med3 == min3, then the literal length of render.frag:105-116).
+__device__ __forceinline__ float march_len(const SunRay &S, float f0, float f1, float f2) {
+    const float x0 = -f0 * S.sign[0], x1 = -f1 * S.sign[1], x2 = -f2 * S.sign[2];     // :94
+    const float d0 = (x0 - floorf(x0)) + 1e-4f;
+    const float d1 = (x1 - floorf(x1)) + 1e-4f;
+    const float d2 = (x2 - floorf(x2)) + 1e-4f;
+    const float t0 = div_const(d0, S.abs[0], S.rcp[0]);                                // :97
+    const float t1 = div_const(d1, S.abs[1], S.rcp[1]);
+    const float t2 = div_const(d2, S.abs[2], S.rcp[2]);
+    float len = __builtin_fminf(__builtin_fminf(t0, t1), t2);                         // :100-105, one axis
+    if (__builtin_amdgcn_fmed3f(t0, t1, t2) == len) {                                  // ties: literal length
+        const float v0 = t0 == len ? t0 : 0.0f, v1 = t1 == len ? t1 : 0.0f, v2 = t2 == len ? t2 : 0.0f;
+        len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    }
+    return len;
+}
+
 __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
                            float f1, float f2, unsigned &fetches) {
     const FrameConsts &F = a.fc;
-    const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
-    const float b0 = S.abs[0], b1 = S.abs[1], b2 = S.abs[2];
-    const float y0 = S.rcp[0], y1 = S.rcp[1], y2 = S.rcp[2];
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
     if (maxs <= 0) return maxs == 0;
     float safe = 1.0f;
     float e0 = (float)c0, e1 = (float)c1, e2 = (float)c2;
+    float len = march_len(S, f0, f1, f2);
     int step = 0;                                                                // wave-uniform
     do {
-        const float x0 = -f0 * s0, x1 = -f1 * s1, x2 = -f2 * s2;                  // :94
-        const float d0 = (x0 - floorf(x0)) + 1e-4f;
-        const float d1 = (x1 - floorf(x1)) + 1e-4f;
-        const float d2 = (x2 - floorf(x2)) + 1e-4f;
-        const float t0 = div_const(d0, b0, y0);                                  // :97
-        const float t1 = div_const(d1, b1, y1);
-        const float t2 = div_const(d2, b2, y2);
-        float len = __builtin_fminf(__builtin_fminf(t0, t1), t2);               // :100-105, one axis
-        if (__builtin_amdgcn_fmed3f(t0, t1, t2) == len) {                        // ties: literal length
-            const float v0 = t0 == len ? t0 : 0.0f, v1 = t1 == len ? t1 : 0.0f, v2 = t2 == len ? t2 : 0.0f;
-            len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
-        }
         f0 = f0 + (r0 * safe) * len;                                             // :118
         f1 = f1 + (r1 * safe) * len;
         f2 = f2 + (r2 * safe) * len;
@@ -172,6 +179,7 @@ __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *
         const bool sky = (unsigned)i0 >= (unsigned)a.X || (unsigned)i1 >= (unsigned)a.Y || (unsigned)i2 >= (unsigned)a.Z;
         const uint32_t t = sun[sky ? 0u : lin_index(a, i0, i1, i2)];             // :123-128
         fetches += sky ? 0u : 1u;
+        len = march_len(S, f0, f1, f2);                                          // next step, under the load
         // safe < 0 marks "lit": left the grid (:123-126), or the step that
         // reaches MAX_STEPS, whatever it read (:234 tests step, not safe)
         safe = sky ? -1.0f : (float)t;
@@ -399,10 +407,9 @@ __device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1
     lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
-    const uint32_t t000 = (uint32_t)a.rg[lin_index(a, x0, y0, z0)], t100 = (uint32_t)a.rg[lin_index(a, x1, y0, z0)];
-    const uint32_t t010 = (uint32_t)a.rg[lin_index(a, x0, y1, z0)], t110 = (uint32_t)a.rg[lin_index(a, x1, y1, z0)];
-    const uint32_t t001 = (uint32_t)a.rg[lin_index(a, x0, y0, z1)], t101 = (uint32_t)a.rg[lin_index(a, x1, y0, z1)];
-    const uint32_t t011 = (uint32_t)a.rg[lin_index(a, x0, y1, z1)], t111 = (uint32_t)a.rg[lin_index(a, x1, y1, z1)];
+    auto ld = [&](int x, int y, int z) -> uint32_t { return (uint32_t)a.rg[lin_index(a, x, y, z)]; };
+    const uint32_t t000 = ld(x0, y0, z0), t100 = ld(x1, y0, z0), t010 = ld(x0, y1, z0), t110 = ld(x1, y1, z0);
+    const uint32_t t001 = ld(x0, y0, z1), t101 = ld(x1, y0, z1), t011 = ld(x0, y1, z1), t111 = ld(x1, y1, z1);
     float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
@@ -418,8 +425,12 @@ __device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1
     return gmin(res[0], res[1]);
 }
 
-__device__ __forceinline__ int wrap_idx(float fl, int n) {
-    const float q = floorf(fl / (float)n);
+// REPEAT wrap of an integer-valued float onto [0, n), n a power of two:
+// floor(fl / n) with the IEEE quotient by n = 2^k, which is exactly fl * 2^-k
+// (fl is 0 or |fl| >= 1: no underflow), so the multiply by rn = 1/n (exact,
+// host-side) replaces a ~10-instruction correctly rounded division.
+__device__ __forceinline__ int wrap_idx(float fl, int n, float rn) {
+    const float q = floorf(fl * rn);
     return f2i(fl - q * (float)n) & (n - 1);
 }
 
@@ -429,7 +440,7 @@ __device__ float fbm(const KernelArgs &a, const float *unorm, float px, float py
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float wa = u - fu, wb = v - fv;
-    const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
+    const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
     const float t00 = unorm[a.noise[(unsigned)y0 * W + x0] >> 24];
     const float t10 = unorm[a.noise[(unsigned)y0 * W + x1] >> 24];
@@ -506,7 +517,7 @@ __device__ void white(const KernelArgs &a, const float *unorm, float px, float p
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float wa = u - fu, wb = v - fv;
-    const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
+    const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
     const uint32_t t00 = a.noise[(unsigned)y0 * W + x0], t10 = a.noise[(unsigned)y0 * W + x1];
     const uint32_t t01 = a.noise[(unsigned)y1 * W + x0], t11 = a.noise[(unsigned)y1 * W + x1];
@@ -753,8 +764,21 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
 // Lane = pixel, wave = 8x8 tile, workgroup = 16x16 pixels.
 // EXT: the extension instantiation (REFLECT, ROUGH, soft shadows); the v1
 // instantiation does not carry their registers or code.
+// Occupancy: 8 waves/SIMD needs <= 64 VGPRs and <= 80 SGPRs (8 256-thread
+// blocks per CU, MI355X_MICROARCH.md "Residency"); the EXT instantiation is
+// held to that budget explicitly (left alone it takes 66 VGPRs + 100 SGPRs
+// and runs at 6 waves/SIMD).
+#ifndef VX_EXT_OCC
+#define VX_EXT_OCC 1
+#endif
+#if VX_EXT_OCC
+#define VX_OCC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_sgpr(80)))
+#else
+#define VX_OCC_ATTR
+#endif
 template <int FMT, bool STATS, bool TILED, bool EXT>
-__global__ __launch_bounds__(256) void k_render(KernelArgs a) {
+__global__ __launch_bounds__(256) VX_OCC_ATTR
+void k_render(KernelArgs a) {
     // unorm8 -> float table: b/255 as IEEE quotients (render.frag:38 decode)
     __shared__ float s_unorm[256];
     s_unorm[threadIdx.x] = (float)threadIdx.x / 255.0f;
