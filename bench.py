@@ -82,10 +82,12 @@ def main():
 
     grid = presets.scene_grid(cfg["scene"])
     Z, Y, X = grid.shape
-    field = vx.field_build(grid)
     noise = vx.noise_synth(0)
-    scene = vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+    t_scene = time.perf_counter()
+    # palette grid in, distance field + octant copies built on the device (f-1)
+    scene = vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
                      noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=local)
+    t_scene = time.perf_counter() - t_scene
     flags = args.flags if args.flags is not None else (vx.FLAG_FULL_QUALITY if args.quality == "full" else 0)
     samples = args.samples if args.samples is not None else cfg.get("samples", 1)
     frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
@@ -209,7 +211,7 @@ def main():
                     f"v1 shading flags={flags}") +
                     (f" + {samples}-sample soft shadows (sun radius {args.sun_radius})" if samples > 1 else "") +
                     f", field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, RGBA8 framebuffer in HBM",
-                "flags": flags, "shadow_samples": samples,
+                "flags": flags, "shadow_samples": samples, "scene_build_s": round(t_scene, 3),
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
                 "tiles": {"size": TILE, "count": n_tiles, "assignment": "round-robin"} if world > 1 else None,
                 "fps": round(1000.0 / ms_per_step, 2),
@@ -232,7 +234,7 @@ def main():
             },
         }
         if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(field, scene, noise, frame, W, H, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(scene, noise, frame, W, H, args.cpu_seconds)
     scene.close()
     if world > 1:
         dist.barrier()
@@ -241,7 +243,7 @@ def main():
         print(json.dumps(result), flush=True)
 
 
-def cpu_baseline(field, scene, noise, frame, W, H, target_s):
+def cpu_baseline(scene, noise, frame, W, H, target_s):
     """The scalar oracle (oracle/, -O2 -fno-fast-math -ffp-contract=off, OpenMP
     over rows) on a bounded sample of the same frame: whole frames repeated
     until ~target_s when a frame is cheap (median rate reported), else a

@@ -40,6 +40,8 @@ extern "C" {
 #define VX_FORMAT_BIN 1     /* raw RGBA8 bytes */
 #define VX_FORMAT_BIN_GZ 2  /* gzip of raw (makefile:70-71) */
 #define VX_FORMAT_BLOB 3    /* AES-256-CBC(PKCS#7, fixed IV) of gzip (encrypt.js:12-46) */
+#define VX_FORMAT_GRID 4    /* map only: raw palette-index grid, X*Y*Z bytes (the input of
+                               sdf.cpp); the distance field is built on the GPU */
 
 /* output pixel formats */
 #define VX_PIXEL_RGBA32F 0  /* 16 B/pixel, parity format */
@@ -174,6 +176,10 @@ int vx_blob_encrypt(const void *in, size_t n, const char *key_jwk_k,
 /* map.bin from a palette-index grid (x fastest): sdf.cpp:405-470.
  * rgba_out holds X*Y*Z*4 bytes; A is written 0 as sdf.cpp:469 does. */
 int vx_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int n_threads);
+
+/* Same output as vx_field_build, computed on GPU `device` (plane-parallel
+ * restatement of the same recurrence; host buffers in and out). */
+int vx_field_build_gpu(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int device);
 
 /* Deterministic synthetic noise texture in noise.bin layout (noise.cpp:34-41). */
 int vx_noise_synth(uint32_t seed, int w, int h, uint8_t *rgba_out);

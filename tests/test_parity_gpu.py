@@ -245,3 +245,41 @@ def test_extensions_baseline_rows(full_scene, noise, cfg, cam, step, kw):
     _compare(img, ref, rows)
     assert st.primary_cap_hits == 0
     assert st.reflect_rays == st.glass_px
+
+
+# ---- f-1: the distance field built on the GPU ----------------------------------
+@pytest.mark.parametrize("name", ["small_a", "small_b", "tall", "s_proc", "s_campus", "s_up3"])
+def test_gpu_field_build_equals_host(name):
+    """vx_field_build_gpu (plane-parallel on the device) == vx_field_build (host
+    restatement, itself checked against the literal serial oracle): every byte,
+    up to the C5 3072x768x96 field."""
+    import voxmap_amd as vx
+    from voxmap_amd import presets, scenes
+    if name == "small_a":
+        grid = scenes.small_proc(3, dims=(96, 48, 16), n_boxes=16, n_glass=4)
+    elif name == "small_b":
+        grid = scenes.small_proc(4, dims=(40, 72, 24), n_boxes=10, n_glass=2)
+    elif name == "tall":          # Z > Y: plane-0 shells clipped by Y
+        grid = scenes.small_proc(9, dims=(33, 12, 40), n_boxes=6, n_glass=1)
+    else:
+        grid = presets.scene_grid(name)
+    want = vx.field_build(grid)
+    got = vx.field_build_gpu(grid)
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+
+
+def test_scene_from_grid_equals_scene_from_field(noise):
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (96, 48, 16)
+    grid = scenes.small_proc(12, dims=dims, n_boxes=14, n_glass=5)
+    field = vx.field_build(grid)
+    with _scene(vx, field, noise, dims) as a, vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID,
+                                                     noise_bytes=noise.tobytes(), noise_format=vx.FORMAT_BIN,
+                                                     dims=dims, device=0) as b:
+        for o in (0, 3, 7):
+            assert np.array_equal(a.read_field(o), b.read_field(o))
+        fr = vx.make_frame((48.0, 24.0, 18.0), (1.1, 0.0, 0.6), 64, 48, flags=vx.FLAG_FULL_QUALITY)
+        ia, _ = a.render(fr)
+        ib, _ = b.render(fr)
+    assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32))

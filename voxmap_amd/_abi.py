@@ -21,7 +21,7 @@ ERROR_NAMES = {
     VX_ESIZE: "VX_ESIZE", VX_EDEVICE: "VX_EDEVICE", VX_ENOMEM: "VX_ENOMEM",
 }
 
-FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB = 0, 1, 2, 3
+FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB, FORMAT_GRID = 0, 1, 2, 3, 4
 PIXEL_RGBA32F, PIXEL_RGBA8 = 0, 1
 FLAG_NO_SHADOW, FLAG_NO_AO, FLAG_NO_CLOUDS, FLAG_PRIMARY_ONLY = 0x1, 0x2, 0x4, 0x8
 FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
@@ -95,6 +95,7 @@ SIGNATURES = [
                                   C.POINTER(C.c_size_t)]),
     ("vx_field_build", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
     ("vx_noise_synth", C.c_int, [C.c_uint32, C.c_int, C.c_int, C.c_void_p]),
+    ("vx_field_build_gpu", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
     ("vx_last_error", C.c_char_p, []),
     ("vx_abi_version", C.c_int, []),
 ]

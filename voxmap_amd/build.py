@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libvoxmap_hip.so")
-SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_kernels.hip"]
+SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_kernels.hip", "vx_field_gpu.hip"]
 ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-Wall", f"--offload-arch={ARCH}"]
 LIBS = ["-lz", "-lcrypto", "-lpthread"]

@@ -118,9 +118,16 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     const size_t field_bytes = (size_t)X * Y * Z * 4, noise_bytes = (size_t)NW * NH * 4;
 
     std::vector<unsigned char> field, noise;
-    int rc = load_asset(d->map_path, d->map_bytes, d->map_size, d->map_format, d->key_jwk_k, field_bytes, "map",
+    const bool from_grid = d->map_format == VX_FORMAT_GRID;
+    int rc = VX_OK;
+    if (from_grid) {   // palette grid: the field is built on the device below
+        if (!d->map_bytes || d->map_size != (size_t)X * Y * Z)
+            return set_error(VX_ESIZE, "map grid: need map_bytes of X*Y*Z palette indices");
+    } else {
+        rc = load_asset(d->map_path, d->map_bytes, d->map_size, d->map_format, d->key_jwk_k, field_bytes, "map",
                         field);
-    if (rc) return rc;
+        if (rc) return rc;
+    }
     if (d->noise_path || d->noise_bytes) {
         rc = load_asset(d->noise_path, d->noise_bytes, d->noise_size, d->noise_format, d->key_jwk_k, noise_bytes,
                         "noise", noise);
@@ -145,12 +152,26 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
-        (e = hipMemcpyAsync(lin, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess ||
+        (!from_grid &&
+         (e = hipMemcpyAsync(lin, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) ||
         (e = hipMemcpyAsync(s->d_noise, noise.data(), noise_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) {
         if (ga) (void)hipFree(ga);
         if (gb) (void)hipFree(gb);
         if (lin) (void)hipFree(lin);
         return fail(set_error(VX_EDEVICE, std::string("scene upload failed: ") + hipGetErrorString(e)));
+    }
+    if (from_grid) {   // sdf.cpp:405-470 on the device, into the linear RGBA upload buffer
+        uint8_t *d_col = nullptr;
+        e = hipMalloc(&d_col, (size_t)X * Y * Z);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_col, d->map_bytes, (size_t)X * Y * Z, hipMemcpyHostToDevice, s->stream);
+        if (e == hipSuccess) e = (hipError_t)field_build_device(d_col, lin, X, Y, Z, s->stream);
+        if (d_col) (void)hipFree(d_col);
+        if (e != hipSuccess) {
+            (void)hipFree(ga);
+            (void)hipFree(gb);
+            (void)hipFree(lin);
+            return fail(set_error(VX_EDEVICE, std::string("device field build failed: ") + hipGetErrorString(e)));
+        }
     }
     // the kernels' arrays: sun channels and AO array from
     // the upload, then per octant its cube sizes into the upload's A channel
@@ -539,5 +560,28 @@ int vx_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out,
 }
 
 int vx_noise_synth(uint32_t seed, int w, int h, uint8_t *rgba_out) { return noise_synth(seed, w, h, rgba_out); }
+
+int vx_field_build_gpu(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int device) {
+    if (!color || !rgba_out || X <= 0 || Y <= 0 || Z <= 0 || X > 65535 || Y > 65535 || Z > 255)
+        return set_error(VX_EINVAL, "vx_field_build_gpu: bad arguments (need 0<X,Y<=65535, 0<Z<=255)");
+    const size_t N = (size_t)X * Y * Z;
+    if (N > (size_t)INT32_MAX) return set_error(VX_EINVAL, "vx_field_build_gpu: grid too large for int32 volume sums");
+    VX_HIP(hipSetDevice(device));
+    uint8_t *d_col = nullptr;
+    uint32_t *d_rgba = nullptr;
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&d_col, N);
+    if (e == hipSuccess) e = hipMalloc(&d_rgba, 4 * N);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_col, color, N, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = (hipError_t)field_build_device(d_col, d_rgba, X, Y, Z, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(rgba_out, d_rgba, 4 * N, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (d_col) (void)hipFree(d_col);
+    if (d_rgba) (void)hipFree(d_rgba);
+    if (st) (void)hipStreamDestroy(st);
+    if (e != hipSuccess) return set_error(VX_EDEVICE, std::string("vx_field_build_gpu: ") + hipGetErrorString(e));
+    return VX_OK;
+}
 
 }  // extern "C"

@@ -102,6 +102,8 @@ int launch_field_unpack(const uint16_t *rg, const uint16_t *prim_copy, uint32_t 
 int launch_render(const KernelArgs &a, int pixel_format, void *stream);
 int launch_detile(const void *tiles, void *frame, int w, int h, int tile_size, int tiles_x,
                   const int *tile_ids, int n_tiles, int pixel_format, void *stream);
+// map.bin texels (A = 0) from a device palette grid (vx_field_gpu.hip)
+int field_build_device(const uint8_t *d_col, uint32_t *d_rgba, int X, int Y, int Z, void *stream);
 // A channel of octant copy `oct` (in place in a linear grid upload)
 int launch_field_octant(uint32_t *field, int X, int Y, int Z, int cap, int oct, uint8_t *scratch_a,
                         uint8_t *scratch_b, void *stream);

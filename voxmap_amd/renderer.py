@@ -222,6 +222,15 @@ def field_build(color_zyx: np.ndarray, n_threads: int = 0) -> np.ndarray:
     return out
 
 
+def field_build_gpu(color_zyx: np.ndarray, device: int = 0) -> np.ndarray:
+    """vx_field_build on GPU ``device`` (same bytes, plane-parallel on the device)."""
+    col = np.ascontiguousarray(color_zyx, dtype=np.uint8)
+    Z, Y, X = col.shape
+    out = np.empty((Z, Y, X, 4), np.uint8)
+    check(lib().vx_field_build_gpu(col.ctypes.data, X, Y, Z, out.ctypes.data, int(device)))
+    return out
+
+
 def noise_synth(seed: int = 0, w: int = 1024, h: int = 1024) -> np.ndarray:
     out = np.empty((h, w, 4), np.uint8)
     check(lib().vx_noise_synth(int(seed), w, h, out.ctypes.data))
