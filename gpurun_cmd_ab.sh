@@ -1,6 +1,5 @@
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "field_build or from_grid" > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --no-cpu > gpurun_out/b3.log 2>&1 || { tail -20 gpurun_out/b3.log; exit 1; }
-grep -o '"ms_per_step": [0-9.]*\|"scene_build_s": [0-9.]*' gpurun_out/b3.log
-timeout -k 10 300 python bench.py --no-cpu --config C5 > gpurun_out/b5.log 2>&1 || { tail -20 gpurun_out/b5.log; exit 1; }
-grep -o '"ms_per_step": [0-9.]*\|"scene_build_s": [0-9.]*' gpurun_out/b5.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+L=build/variants
+AB_FLAGS="0 48" bash tools/ab.sh pad0:VOXMAP_LIB=$L/pad0.so pad1:VOXMAP_LIB=$L/pad1.so pad0:VOXMAP_LIB=$L/pad0.so pad1:VOXMAP_LIB=$L/pad1.so || exit 1
+AB_FLAGS="48" AB_ARGS="--config C5" bash tools/ab.sh c5pad0:VOXMAP_LIB=$L/pad0.so c5pad1:VOXMAP_LIB=$L/pad1.so

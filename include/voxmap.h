@@ -116,6 +116,8 @@ typedef struct vx_stats {
     uint64_t primary_cap_hits;  /* must be 0 */
     uint64_t reflect_rays, reflect_fetches;   /* ext REFLECT: reflection rays traced, texels read */
     uint64_t rough_px;          /* ext ROUGH: fragments with a jittered normal (4 noise texels each) */
+    uint64_t primary_wave_iters, march_wave_iters;   /* diagnostic: loop iterations summed over
+                                   waves; lane utilisation = fetches / (64 * wave_iters) */
     uint64_t alg_bytes;         /* 4*(primary+shadow+reflect fetches) + 32*ao + 80*clouded sky
                                    + 16*rough + out bytes */
     double kernel_ms;           /* HIP-event time of the render kernel(s) */

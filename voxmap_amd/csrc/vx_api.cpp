@@ -42,6 +42,8 @@ struct vx_scene {
     int noise_w = 0, noise_h = 0;
     uint16_t *d_prim = nullptr;   // 8 padded octant copies (vx_internal.h FieldLayout)
     uint8_t *d_sun = nullptr;     // R, G channels
+    int8_t *d_sunp = nullptr;     // R, G channels, int8, -1 border (Z <= 126)
+    int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
     uint32_t *d_noise = nullptr;
     unsigned long long *d_stats = nullptr;
@@ -182,6 +184,17 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMalloc(&s->d_sun, 2 * N)) == hipSuccess && (e = hipMalloc(&s->d_rg, 2 * N)) == hipSuccess &&
         (e = hipMemsetD16Async((hipDeviceptr_t)s->d_prim, 0xFF00u, 8 * L.texels, s->stream)) == hipSuccess) {
         lrc = launch_field_pack(lin, nullptr, s->d_sun, s->d_rg, X, Y, Z, L.pad, s->stream);
+        // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
+        // march's loaded value carries the exit test (vx_kernels.hip march_fast); values <= Z <= 126
+        if (!lrc && Z <= 126 && (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2)) < (1u << 24)) {
+            s->SB = Z + 2;
+            s->SXp = X + 2 * s->SB; s->SYp = Y + 2 * s->SB; s->SZp = Z + 2 * s->SB;
+            const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
+            if ((e = hipMalloc(&s->d_sunp, 2 * np)) == hipSuccess &&
+                (e = hipMemsetAsync(s->d_sunp, 0xFF, 2 * np, s->stream)) == hipSuccess)
+                lrc = launch_sun_pad(lin, s->d_sunp, X, Y, Z, s->SB, s->stream);
+            if (e != hipSuccess) lrc = (int)e;
+        }
         for (int oct = 0; oct < 8 && !lrc; oct++) {
             lrc = launch_field_octant(lin, X, Y, Z, cap, oct, ga, gb, s->stream);
             if (!lrc) lrc = launch_field_pack(lin, s->d_prim + oct * L.texels, nullptr, nullptr, X, Y, Z, L.pad, s->stream);
@@ -205,6 +218,7 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->d_prim) (void)hipFree(s->d_prim);
     if (s->d_sun) (void)hipFree(s->d_sun);
+    if (s->d_sunp) (void)hipFree(s->d_sunp);
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
@@ -278,6 +292,8 @@ static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int 
     st->reflect_rays = v[ST_REFL_RAYS];
     st->reflect_fetches = v[ST_REFL_FETCH];
     st->rough_px = v[ST_ROUGH];
+    st->primary_wave_iters = v[ST_PRIM_WITERS];
+    st->march_wave_iters = v[ST_MARCH_WITERS];
     // 4 B per field texel read (primary, shadow and reflection
     // rays), 32 B per trilinear AO, 80 B per clouded sky pixel (5 bilinear
     // noise taps), 16 B per rough-normal white() tap (4 texels), plus the
@@ -295,6 +311,11 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     std::memset(&a, 0, sizeof a);
     a.prim = s->d_prim;
     a.sun = s->d_sun;
+    a.sunp = s->d_sunp;
+    a.SB = s->SB;
+    a.SXp = s->SXp;
+    a.SXpYp = (unsigned)s->SXp * (unsigned)s->SYp;
+    a.sunp_texels = a.SXpYp * (unsigned)s->SZp;
     a.rg = s->d_rg;
     a.noise = s->d_noise;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;

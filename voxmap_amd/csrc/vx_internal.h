@@ -52,6 +52,10 @@ struct FrameConsts {
 struct KernelArgs {
     const uint16_t *prim;    // 8 padded octant copies: colour | cube size << 8 (FieldLayout)
     const uint8_t *sun;      // R channel then G channel, X*Y*Z bytes each
+    const int8_t *sunp;      // R then G, int8, inside a border of SB cells of -1 (nullptr: Z > 126)
+    int SB;                  // border width of sunp (Z + 2: a march step moves <= Z + 1 cells per axis)
+    int SXp;                 // padded row length of sunp
+    unsigned SXpYp, sunp_texels;
     const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *noise;   // RGBA8 noise texels
     int X, Y, Z;
@@ -79,7 +83,7 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
 
 enum StatSlot {
     ST_PIXELS = 0, ST_SKY, ST_BLOCK, ST_GLASS, ST_PRIM_FETCH, ST_SHADOW_RAYS, ST_SHADOW_FETCH,
-    ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_REFL_RAYS, ST_REFL_FETCH, ST_ROUGH, ST_COUNT
+    ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_REFL_RAYS, ST_REFL_FETCH, ST_ROUGH, ST_PRIM_WITERS, ST_MARCH_WITERS, ST_COUNT
 };
 
 // Field data in HBM (vx_kernels.hip): `prim` = 8 copies (one
@@ -91,6 +95,8 @@ struct FieldLayout {
     size_t texels;           // Xp * Yp * Zp, one prim copy
 };
 FieldLayout field_layout(int X, int Y, int Z, int cap);
+// padded int8 sun channels (border = -1) from the linear RGBA upload
+int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int SB, void *stream);
 // linear RGBA upload (A = an octant's cube sizes) -> prim copy; -> sun, rg (either may be null)
 int launch_field_pack(const uint32_t *lin, uint16_t *prim_copy, uint8_t *sun, uint16_t *rg, int X, int Y, int Z,
                       int pad, void *stream);

@@ -21,6 +21,20 @@
 
 #include "vx_internal.h"
 
+// Diagnostic padding (A/B only, never in the product build): VX_PAD_MARCH /
+// VX_PAD_PRIM extra independent v_add_f32 per loop iteration.
+#ifndef VX_MARCH_PAD
+#define VX_MARCH_PAD 1
+#endif
+#ifndef VX_PAD_MARCH
+#define VX_PAD_MARCH 0
+#endif
+#ifndef VX_PAD_PRIM
+#define VX_PAD_PRIM 0
+#endif
+#define VX_PAD(N, ACC)                                                        \
+    _Pragma("unroll") for (int pad_i = 0; pad_i < (N); pad_i++) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(ACC));
+
 namespace vx {
 namespace {
 
@@ -106,7 +120,14 @@ struct Surf {            // one G-buffer record (what render.vert hands render.f
 struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
     unsigned refl_rays, refl_fetch, rough;   // extensions
+    unsigned prim_witers, march_witers;      // loop iterations per wave (diagnostic: lane utilisation)
 };
+
+// v counted once per wave: by the first active lane (wave-uniform loop counts)
+__device__ __forceinline__ unsigned once_per_wave(unsigned v) {
+    const unsigned long long act = __ballot(1);
+    return __lane_id() == (unsigned)(__ffsll((unsigned long long)act) - 1) ? v : 0u;
+}
 
 // Field data in HBM, each array shaped for the loop that
 // reads it, so a cache line holds as many useful cells as possible:
@@ -159,7 +180,7 @@ __device__ __forceinline__ float march_len(const SunRay &S, float f0, float f1, 
 }
 
 __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
-                           float f1, float f2, unsigned &fetches) {
+                           float f1, float f2, unsigned &fetches, unsigned &witers) {
     const FrameConsts &F = a.fc;
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
@@ -168,7 +189,9 @@ __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *
     float e0 = (float)c0, e1 = (float)c1, e2 = (float)c2;
     float len = march_len(S, f0, f1, f2);
     int step = 0;                                                                // wave-uniform
+    float pad_acc = 0.0f;
     do {
+        VX_PAD(VX_PAD_MARCH, pad_acc)
         f0 = f0 + (r0 * safe) * len;                                             // :118
         f1 = f1 + (r1 * safe) * len;
         f2 = f2 + (r2 * safe) * len;
@@ -185,13 +208,67 @@ __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *
         safe = sky ? -1.0f : (float)t;
         if (++step >= maxs) safe = -1.0f;
     } while (safe > 0.0f);
+    witers += once_per_wave((unsigned)step);
+    if (VX_PAD_MARCH) asm volatile("" ::"v"(pad_acc));
     return safe < 0.0f;
+}
+
+// The same march over the int8 sun channels inside a border of -1 cells
+// (vx_scene_create, Z <= 126): a step moves at most safe + 1 <= Z + 1 cells
+// per axis, so the texel a lane loads after leaving the grid is a border
+// cell and its -1 is the exit ("lit", render.frag:123-126) -- no bounds test.
+// Cells are padded-grid fp32 integers; the index x + Xp*y is one exact fp32
+// fma (< 2^24, checked on the host), then + XpYp*z in integers.  The last
+// step (step MAX_STEPS-1 -> MAX_STEPS) is lit whatever it reads (:234), so
+// the loop runs MAX_STEPS-1 steps with the step test on the scalar unit, and
+// a lane still marching afterwards is lit.
+__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1, int c2, float f0,
+                          float f1, float f2, unsigned &fetches, unsigned &witers) {
+    const FrameConsts &F = a.fc;
+    const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
+    const int maxs = F.max_steps;
+    if (maxs <= 0) return maxs == 0;
+    const float xpf = (float)a.SXp;
+    float e0 = (float)(c0 + a.SB), e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB);
+    float safe = 1.0f;
+    float len = march_len(S, f0, f1, f2);
+    const unsigned sxpyp = a.SXpYp;
+    // one step of :94-128 -> the texel (-1: left the grid)
+#define VX_PAD_STEP(T)                                                                        \
+    {                                                                                         \
+        f0 = f0 + (r0 * safe) * len; /* :118 */                                              \
+        f1 = f1 + (r1 * safe) * len;                                                          \
+        f2 = f2 + (r2 * safe) * len;                                                          \
+        const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);                     \
+        e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                                   \
+        f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2; /* :120 */                               \
+        const unsigned xy = (unsigned)__builtin_fmaf(e1, xpf, e0); /* exact: < 2^24 */        \
+        T = sun[__umul24((unsigned)e2, sxpyp) + xy]; /* :123-128 */                           \
+        fetches += T >= 0 ? 1u : 0u;                                                          \
+    }
+    int step = 0;                                                                // wave-uniform
+    if (maxs > 1) {
+        do {
+            int t;
+            VX_PAD_STEP(t)
+            len = march_len(S, f0, f1, f2);                                      // next step, under the load
+            safe = (float)t;
+        } while (safe > 0.0f && ++step < maxs - 1);
+    }
+    witers += once_per_wave((unsigned)step + 1u);
+    if (safe > 0.0f) {                         // the MAX_STEPS-th step: only its fetch (stats) matters
+        int t;
+        VX_PAD_STEP(t)
+        (void)t;
+    }
+#undef VX_PAD_STEP
+    return safe != 0.0f;
 }
 
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
 __device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
-                              float f1, float f2, unsigned &fetches) {
+                              float f1, float f2, unsigned &fetches, unsigned &witers) {
     const FrameConsts &F = a.fc;
     const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
     const float a0 = S.abs[0], a1 = S.abs[1], a2 = S.abs[2];
@@ -216,21 +293,30 @@ __device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_
         const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
         c0 += f2i(fl0); c1 += f2i(fl1); c2 += f2i(fl2);
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;
-        if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) return true;
+        if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) {
+            witers += once_per_wave((unsigned)step + 1u);
+            return true;
+        }
         const uint32_t t = sun[lin_index(a, c0, c1, c2)];
         fetches++;
         safe = (float)t;
         step++;
     }
+    witers += once_per_wave((unsigned)step);
     return step == maxs;
 }
 
-// march(cell, fract, S.r) of render.frag:233 -> "lit" (step == MAX_STEPS, :234)
-__device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay &S, int c0, int c1, int c2, float f0,
-                                          float f1, float f2, unsigned &fetches) {
+// march(cell, fract, S.r) of render.frag:233 -> "lit" (step == MAX_STEPS, :234).
+// S by value: the soft-shadow loop indexes sun_k[k] dynamically, and a
+// reference into the kernel argument there made the compiler copy the whole
+// KernelArgs (1.5 KB) to scratch.
+__device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
+                                          float f1, float f2, unsigned &fetches, unsigned &witers) {
+    if (VX_MARCH_PAD && S.fast && a.sunp)
+        return march_pad(a, S, S.up ? a.sunp : a.sunp + a.sunp_texels, c0, c1, c2, f0, f1, f2, fetches, witers);
     const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
-    return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, fetches)
-                  : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, fetches);
+    return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers)
+                  : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers);
 }
 
 // ---------------- primary visibility ----------------
@@ -308,7 +394,9 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
     // the first glass entry); the step counter is wave-uniform.
     const int cap = 4 * (a.X + a.Y + a.Z);
     int it = 0;
+    float pad_acc = 0.0f;
     do {
+        VX_PAD(VX_PAD_PRIM, pad_acc)
         const f2 Rv = {R, R};
         const f2 Axy = __builtin_elementwise_fma(sxy, Rv, hxy);
         const float Az = __builtin_fmaf(sz, R, hz);
@@ -349,6 +437,8 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
         prev = col;
         R = (float)(t >> 8);
     } while (stop == 0 && ++it < cap);
+    cnt.prim_witers += once_per_wave((unsigned)it + 1u);
+    if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
     asm volatile("" : "+v"(col));
     if (stop == 0) cnt.cap_hit++;
     const bool hit = stop != 0 && t < kSentinel;
@@ -586,13 +676,13 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
         if (!EXT || F.n_sun <= 1) {
             cnt.shadow_rays++;
-            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch);
+            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch, cnt.march_witers);
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
         } else {                       // ext soft shadows: lit fraction of the sun samples
             int lit = 0;
             for (int k = 0; k < F.n_sun; k++) {
                 cnt.shadow_rays++;
-                lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch) ? 1 : 0;
+                lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch, cnt.march_witers) ? 1 : 0;
             }
             shadeFactor = shadeFactor * ((float)lit / (float)F.n_sun);
         }
@@ -802,7 +892,7 @@ void k_render(KernelArgs a) {
     }
     const int px = ox + lx, py = oy + ly;
     const FrameConsts &F = a.fc;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
     if (px < a.w && py < a.h) {
         float d0, d1, d2;
@@ -868,6 +958,8 @@ void k_render(KernelArgs a) {
         v[ST_REFL_RAYS] = wave_sum(cnt.refl_rays);
         v[ST_REFL_FETCH] = wave_sum(cnt.refl_fetch);
         v[ST_ROUGH] = wave_sum(cnt.rough);
+        v[ST_PRIM_WITERS] = wave_sum(cnt.prim_witers);
+        v[ST_MARCH_WITERS] = wave_sum(cnt.march_witers);
         if (lane == 0) {
             // spread the adds over 64 slot rows to avoid one hot line per counter
             unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
@@ -988,6 +1080,17 @@ __global__ void k_pack_sun(const uint32_t *src, uint8_t *sun, uint16_t *rg, size
     sun[N + i] = (uint8_t)((t >> 8) & 0xffu);
     rg[i] = (uint16_t)(t & 0xffffu);
 }
+// linear RGBA upload -> the padded int8 sun channels (border pre-filled with -1)
+__global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z, int SB) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)X * Y * Z) return;
+    const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+    const size_t Xp = (size_t)X + 2 * SB, Yp = (size_t)Y + 2 * SB, Zp = (size_t)Z + 2 * SB;
+    const size_t j = (size_t)(x + SB) + Xp * ((size_t)(y + SB) + Yp * (size_t)(z + SB));
+    const uint32_t t = src[i];
+    sunp[j] = (int8_t)(t & 0xffu);
+    sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);
+}
 // RGBA of one octant copy (R, G from rg; B, A from prim) for vx_scene_read_field_copy
 __global__ void k_unpack(const uint16_t *rg, const uint16_t *prim, uint32_t *dst, int X, int Y, int Z, int P) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1015,6 +1118,13 @@ int launch_field_pack(const uint32_t *lin, uint16_t *prim_copy, uint8_t *sun, ui
     const dim3 grid((unsigned)((N + 255) / 256)), block(256);
     if (prim_copy) hipLaunchKernelGGL(k_pack_prim, grid, block, 0, (hipStream_t)stream, lin, prim_copy, X, Y, Z, pad);
     if (sun) hipLaunchKernelGGL(k_pack_sun, grid, block, 0, (hipStream_t)stream, lin, sun, rg, N);
+    return (int)hipGetLastError();
+}
+
+int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int SB, void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    hipLaunchKernelGGL(k_sun_pad, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lin, sunp, X, Y,
+                       Z, SB);
     return (int)hipGetLastError();
 }
 
