@@ -38,6 +38,12 @@ def test_error_paths_do_not_touch_the_gpu(built):
     with pytest.raises(vx.VoxmapError) as e:
         vx.Scene(map_bytes=b"\x00" * 256, map_format=vx.FORMAT_BIN, dims=(4, 4, 4), dist_cap=300)
     assert e.value.code == -1
+    with pytest.raises(vx.VoxmapError) as e:   # palette index 255 = the traversal's border sentinel
+        vx.Scene(map_bytes=bytes([0, 0, 255, 0]) * 64, map_format=vx.FORMAT_BIN, dims=(4, 4, 4))
+    assert e.value.code == -1 and "reserved" in str(e.value)
+    with pytest.raises(vx.VoxmapError) as e:
+        vx.Scene(map_bytes=b"\xff" * 64, map_format=vx.FORMAT_GRID, dims=(4, 4, 4))
+    assert e.value.code == -1
     with pytest.raises(vx.VoxmapError) as e:
         vx.decode(b"\x1f\x8bnot really gzip", vx.FORMAT_BIN_GZ)
     assert e.value.code == -3

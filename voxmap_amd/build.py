@@ -3,6 +3,7 @@
 Flags that are part of the numerical contract:
   -ffp-contract=off      no FMA contraction (HIP's default is fast-honor-pragmas)
   (default) -fhip-fp32-correctly-rounded-divide-sqrt  IEEE fp32 / and sqrt
+(-fno-slp-vectorize is a speed flag: it does not change fp32 results.)
 """
 from __future__ import annotations
 
@@ -15,7 +16,9 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libvoxmap_hip.so")
 SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_kernels.hip", "vx_field_gpu.hip"]
 ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-Wall", f"--offload-arch={ARCH}"]
+# -fno-slp-vectorize: packed FP32 (v_pk_*) issues at the cost of two scalar ops
+# on gfx950 (profiles/r01_valu_costs.txt), so SLP packing only adds moves.
+FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", f"--offload-arch={ARCH}"]
 LIBS = ["-lz", "-lcrypto", "-lpthread"]
 
 
@@ -35,14 +38,14 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True, out: str | None = None, defines=()) -> str:
+def build(force: bool = False, verbose: bool = True, out: str | None = None, defines=(), extra_flags=()) -> str:
     """Build the library.  ``out``/``defines`` make experiment variants (A/B runs
     select one with VOXMAP_LIB=path); the product is always the default build."""
     target = out or OUT
-    if out is None and not defines and not force and not needs_build():
+    if out is None and not defines and not extra_flags and not force and not needs_build():
         return OUT
     tmp = target + ".tmp"
-    cmd = [hipcc(), *FLAGS, *[f"-D{d}" for d in defines], "-shared", "-o", tmp,
+    cmd = [hipcc(), *FLAGS, *extra_flags, *[f"-D{d}" for d in defines], "-shared", "-o", tmp,
            *[os.path.join(CSRC, s) for s in SOURCES], *LIBS]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -130,6 +130,12 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
                         field);
         if (rc) return rc;
     }
+    {   // palette index 0xFF is the traversal's border sentinel (vx_kernels.hip primary())
+        const unsigned char *col = from_grid ? static_cast<const unsigned char *>(d->map_bytes) : field.data() + 2;
+        const size_t stride = from_grid ? 1 : 4, n = (size_t)X * Y * Z;
+        for (size_t i = 0; i < n; i++)
+            if (col[i * stride] == 0xFF) return set_error(VX_EINVAL, "map: palette index 255 is reserved");
+    }
     if (d->noise_path || d->noise_bytes) {
         rc = load_asset(d->noise_path, d->noise_bytes, d->noise_size, d->noise_format, d->key_jwk_k, noise_bytes,
                         "noise", noise);
@@ -182,7 +188,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     int lrc = 0;
     if ((e = hipMalloc(&s->d_prim, 8 * L.texels * 2)) == hipSuccess &&
         (e = hipMalloc(&s->d_sun, 2 * N)) == hipSuccess && (e = hipMalloc(&s->d_rg, 2 * N)) == hipSuccess &&
-        (e = hipMemsetD16Async((hipDeviceptr_t)s->d_prim, 0xFF00u, 8 * L.texels, s->stream)) == hipSuccess) {
+        (e = hipMemsetD16Async((hipDeviceptr_t)s->d_prim, 0xFFFFu, 8 * L.texels, s->stream)) == hipSuccess) {
         lrc = launch_field_pack(lin, nullptr, s->d_sun, s->d_rg, X, Y, Z, L.pad, s->stream);
         // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
         // march's loaded value carries the exit test (vx_kernels.hip march_fast); values <= Z <= 126

@@ -132,7 +132,7 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 // Field data in HBM, each array shaped for the loop that
 // reads it, so a cache line holds as many useful cells as possible:
 //   prim  8 copies, one per ray octant, u16 per cell: colour | air-cube size
-//         << 8, inside a border of P = cap sentinel cells (0xFF00: size 255,
+//         << 8, inside a border of P = cap sentinel cells (0xFFFF: size 255,
 //         never real, sizes are <= cap - 1 <= 254), so the primary traversal
 //         detects leaving the grid from the value it loads;
 //   sun   map.bin's R ("up") and G ("down") channels, u8 each, linear: the
@@ -140,7 +140,7 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 //   rg    R | G << 8, u16, linear: the AO trilinear sample.
 // Every read is in bounds: the traversal stays within P of the grid, march()
 // returns before reading outside it, the AO sample clamps.
-constexpr uint32_t kSentinel = 0xFF00u;
+constexpr uint32_t kSentinel = 0xFF00u;   // border cells hold 0xFFFF: size 255, colour 0xFF
 
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
 __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
@@ -367,13 +367,9 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
     const int c2 = min(max((int)floorf(o2 + tlo * d2), -cc2), a.Z - cc2 - 1);
     const bool p0 = !(d0 < 0.0f), p1 = !(d1 < 0.0f), p2 = !(d2 < 0.0f);
     const int ip0 = p0, ip1 = p1, ip2 = p2;
-    const f2 sxy = {p0 ? 1.0f : -1.0f, p1 ? 1.0f : -1.0f};
-    const float sz = p2 ? 1.0f : -1.0f;
-    const f2 hpxy = {(float)ip0, (float)ip1}, hmxy = {(float)(ip0 - 1), (float)(ip1 - 1)};
-    const float hpz = (float)ip2, hmz = (float)(ip2 - 1);
-    const f2 oxy = {o0, o1}, dxy = {d0, d1}, ivxy = {iv0, iv1};
-    f2 hxy = {(float)(c0 + ip0), (float)(c1 + ip1)};
-    float hz = (float)(c2 + ip2);
+    const float s0 = p0 ? 1.0f : -1.0f, s1 = p1 ? 1.0f : -1.0f, s2 = p2 ? 1.0f : -1.0f;
+    const float hp0 = (float)ip0, hp1 = (float)ip1, hp2 = (float)ip2;
+    float h0 = (float)(c0 + ip0), h1 = (float)(c1 + ip1), h2 = (float)(c2 + ip2);
     // padded index of h: kray + hx + Xp*hy + XpYp*hz, mod 2^32 with 24-bit
     // signed products (|h| < 2^23)
     const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
@@ -381,73 +377,66 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
         return (uint32_t)ppad[(unsigned)idx];
     };
-    uint32_t t = fetch(hxy.x, hxy.y, hz);
+    uint32_t t = fetch(h0, h1, h2);
     cnt.prim_fetch++;
     int prev = t & 0xff;
-    float R = (float)(t >> 8);
-    // ints, not bools: loop-carried and live-out lane masks cost SALU merges per step
-    int have_glass = 0, stop;
-    f2 gxy = {0.0f, 0.0f};
-    float gz = 0.0f, gt = 0.0f, te;
-    int gax = 0, hax, col;
-    // One exit test per step (a sentinel texel, or a colour change that is not
-    // the first glass entry); the step counter is wave-uniform.
+    float R = (float)((t >> 8) & 0xffu);
+    // gmark: the colour whose entry is "the first glass" -- glass until a glass
+    // entry is recorded, then 256 (matches nothing).  The sentinel's colour
+    // byte 0xFF is no palette index (vx_scene_create), so leaving the grid is
+    // a colour change and the step has a single test: change && !first glass.
+    int gmark = kGlass, stop, col;
+    float g0h = 0.0f, g1h = 0.0f, g2h = 0.0f, gt = 0.0f, te;
+    float tb0, tb1, tb2;
+    int gax = 0;
     const int cap = 4 * (a.X + a.Y + a.Z);
     int it = 0;
     float pad_acc = 0.0f;
     do {
         VX_PAD(VX_PAD_PRIM, pad_acc)
-        const f2 Rv = {R, R};
-        const f2 Axy = __builtin_elementwise_fma(sxy, Rv, hxy);
-        const float Az = __builtin_fmaf(sz, R, hz);
-        const f2 tbxy = (Axy - oxy) * ivxy;
-        const float tbz = (Az - o2) * iv2;
-        te = __builtin_fminf(__builtin_fminf(tbxy.x, tbxy.y), tbz);
-        const bool e0 = tbxy.x == te;
-        const bool e1 = !e0 && tbxy.y == te;
-        const bool e2 = !e0 && !e1;
-        const f2 tev = {te, te};
-        const f2 pxy = oxy + tev * dxy;
-        const float pz = o2 + te * d2;
-        const f2 fxy = {floorf(pxy.x), floorf(pxy.y)};
-        const f2 qxy = fxy + hpxy;
-        const float qz = floorf(pz) + hpz;
-        const f2 loxy = __builtin_elementwise_fma(hmxy, Rv, hxy), hixy = __builtin_elementwise_fma(hpxy, Rv, hxy);
-        const f2 xxy = Axy + sxy;
-        const float xz = Az + sz;
-        const float n0 = e0 ? xxy.x : __builtin_amdgcn_fmed3f(qxy.x, loxy.x, hixy.x);
-        const float n1 = e1 ? xxy.y : __builtin_amdgcn_fmed3f(qxy.y, loxy.y, hixy.y);
-        const float n2 = e2 ? xz : __builtin_amdgcn_fmed3f(qz, __builtin_fmaf(hmz, R, hz), __builtin_fmaf(hpz, R, hz));
-        hxy = (f2){n0, n1};
-        hz = n2;
-        hax = e0 ? 0 : (e1 ? 1 : 2);
-        asm volatile("" : "+v"(hax));                  // keep e0/e1 from living past the loop
-        t = fetch(n0, n1, n2);
-        const bool oob = t >= kSentinel;               // left the grid: sky behind
-        cnt.prim_fetch += oob ? 0u : 1u;
+        // far face of the air cube [c, c + R*s] ahead: A = h + s*R (exact)
+        const float A0 = __builtin_fmaf(s0, R, h0), A1 = __builtin_fmaf(s1, R, h1), A2 = __builtin_fmaf(s2, R, h2);
+        tb0 = (A0 - o0) * iv0;
+        tb1 = (A1 - o1) * iv1;
+        tb2 = (A2 - o2) * iv2;
+        te = __builtin_fminf(__builtin_fminf(tb0, tb1), tb2);
+        const bool e0 = tb0 == te;
+        const bool e1 = !e0 && tb1 == te;
+        // other axes: floor(o + te*d) as h, clamped into the cube, whose h
+        // range is [h, A] (positive axis) or [A, h] (negative): med3(q, h, A)
+        const float q0 = floorf(o0 + te * d0) + hp0;
+        const float q1 = floorf(o1 + te * d1) + hp1;
+        const float q2 = floorf(o2 + te * d2) + hp2;
+        h0 = e0 ? A0 + s0 : __builtin_amdgcn_fmed3f(q0, h0, A0);
+        h1 = e1 ? A1 + s1 : __builtin_amdgcn_fmed3f(q1, h1, A1);
+        h2 = (!e0 && !e1) ? A2 + s2 : __builtin_amdgcn_fmed3f(q2, h2, A2);
+        t = fetch(h0, h1, h2);
+        cnt.prim_fetch += t >= kSentinel ? 0u : 1u;
         col = t & 0xff;
-        const bool change = col != prev && !oob;
-        const bool gfirst = change && col == kGlass && have_glass == 0;
+        const bool change = col != prev;
+        const bool gfirst = change && col == gmark;
         if (gfirst) {                                  // glass: blend over the next surface
-            have_glass = 1;
-            gxy = hxy; gz = hz; gt = te; gax = hax;
+            gmark = 256;
+            g0h = h0; g1h = h1; g2h = h2; gt = te;
+            gax = e0 ? 0 : (e1 ? 1 : 2);
         }
-        stop = (oob || (change && !gfirst)) ? 1 : 0;
-        asm volatile("" : "+v"(stop));
+        stop = (change && !gfirst) ? 1 : 0;
+        asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
         prev = col;
-        R = (float)(t >> 8);
+        R = (float)((t >> 8) & 0xffu);
     } while (stop == 0 && ++it < cap);
     cnt.prim_witers += once_per_wave((unsigned)it + 1u);
     if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
     asm volatile("" : "+v"(col));
     if (stop == 0) cnt.cap_hit++;
     const bool hit = stop != 0 && t < kSentinel;
+    const int hax = tb0 == te ? 0 : (tb1 == te ? 1 : 2);    // exit axis of the last step (ties x < y < z)
     // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
     int nrec = 0;
-    if (have_glass) {
+    if (gmark != kGlass) {
         const bool pos = gax == 0 ? p0 : (gax == 1 ? p1 : p2);
         const int up = pos ? 0 : 1;
-        const float r0 = gxy.x - hpxy.x, r1 = gxy.y - hpxy.y, r2 = gz - hpz;   // relative cell
+        const float r0 = g0h - hp0, r1 = g1h - hp1, r2 = g2h - hp2;   // relative cell
         g0.id = 2;
         g0.color = kGlass;
         g0.nidx = 2 * gax + (pos ? 1 : 0);
@@ -460,10 +449,10 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
         nrec = 1;
     }
     if (hit) {
-        Surf &h = have_glass ? g1 : g0;
+        Surf &h = gmark != kGlass ? g1 : g0;
         const bool pos = hax == 0 ? p0 : (hax == 1 ? p1 : p2);
         const int up = pos ? 0 : 1;
-        const float r0 = hxy.x - hpxy.x, r1 = hxy.y - hpxy.y, r2 = hz - hpz;
+        const float r0 = h0 - hp0, r1 = h1 - hp1, r2 = h2 - hp2;
         h.id = col == kGlass ? 2 : 0;
         h.color = col;
         h.nidx = 2 * hax + (pos ? 1 : 0);
