@@ -2,6 +2,9 @@
  * (DESIGN.md §5): for a divisor a with y = RN(1/a),
  *   q0 = RN(d*y); r0 = fma(-q0,a,d); q1 = fma(r0,y,q0); r1 = fma(-q1,a,d); q2 = fma(r1,y,q1)
  * must equal the IEEE quotient RN(d/a) for every float d in [1e-4, 1.0002].
+ * The one-correction quotient q1 is counted too (the kernels use q1 since
+ * this check found it exact: Markstein's theorem with y = RN(1/a), q0
+ * faithful).  Divisors: a few fixed, 32 adversarial mantissas, then random.
  * Build: gcc -O2 -mfma -ffp-contract=off -fopenmp markstein_check.c -lm */
 #include <math.h>
 #include <stdint.h>
@@ -22,6 +25,11 @@ int main(int argc, char **argv) {
         if (k == 0) a = 0.7287353f; else if (k == 1) a = 0.42073548f; else if (k == 2) a = 0.5403023f;
         else if (k == 3) a = 1.0f; else if (k == 4) a = 0.5f; else if (k == 5) a = u2f(0x3f7fffff);
         else if (k == 6) a = u2f(0x3f000001); else if (k == 7) a = 1e-3f; else if (k == 8) a = 3e-7f;
+        /* adversarial mantissas: all ones, one ulp above/below powers of two, alternating bits */
+        else if (k < 9 + 32) {
+            static const uint32_t m[8] = {0x7fffff, 0x000001, 0x7ffffe, 0x000002, 0x555555, 0x2aaaaa, 0x400000, 0x3fffff};
+            a = u2f(((uint32_t)(100 + (k - 9) / 8 * 7) << 23) | m[(k - 9) % 8]);
+        }
         else a = u2f(0x30000000u + (uint32_t)(((unsigned long long)rand() * 2654435761ull) % 0x0f800000u));
         float y = 1.0f / a;
         unsigned long long bad = 0, bad1 = 0, n = 0;

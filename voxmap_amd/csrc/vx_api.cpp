@@ -328,6 +328,8 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.noise_w = s->noise_w; a.noise_h = s->noise_h;
     a.noise_rw = 1.0f / (float)s->noise_w;   // powers of two: exact
     a.noise_rh = 1.0f / (float)s->noise_h;
+    a.noise_lw = 0;
+    while ((1 << a.noise_lw) < s->noise_w) a.noise_lw++;
     a.w = w; a.h = h;
     a.tile_size = ts;
     a.tiles_x = ts ? (w + ts - 1) / ts : 0;

@@ -61,6 +61,7 @@ struct KernelArgs {
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
     float noise_rw, noise_rh;    // 1/noise_w, 1/noise_h (exact)
+    int noise_lw;                // log2(noise_w)
     int w, h;                // frame size
     int tile_size;           // tiled mode: tile edge in pixels (multiple of 16)
     int tiles_x;             // ceil(w / tile_size)

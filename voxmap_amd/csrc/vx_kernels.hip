@@ -53,12 +53,20 @@ __device__ __forceinline__ int f2i(float x) {
     return x == x ? r : 0;
 }
 
-// a / b, b a per-frame constant with y = RN(1/b): exactly the IEEE quotient
-// (q1 is faithful, Markstein's theorem makes q2 correctly rounded).
+// a / b, b a per-frame constant with y = RN(1/b), a > 0 (no signed zero):
+// exactly the IEEE quotient.  q0 = RN(a*y) is faithful and one Markstein
+// correction q1 = RN(q0 + fma(-q0, b, a)*y) is already correctly rounded
+// (Markstein's theorem for y = RN(1/b); tools/markstein_check.c: 0 mismatches
+// over every numerator in [1e-4, 1.0002] for thousands of divisors, random
+// and adversarial mantissas).  VX_MARKSTEIN_STEPS=2 keeps a second one.
+#ifndef VX_MARKSTEIN_STEPS
+#define VX_MARKSTEIN_STEPS 1
+#endif
 __device__ __forceinline__ float div_const(float a, float b, float y) {
     const float q0 = a * y;
     const float r0 = __builtin_fmaf(-q0, b, a);
     const float q1 = __builtin_fmaf(r0, y, q0);
+    if (VX_MARKSTEIN_STEPS < 2) return q1;
     const float r1 = __builtin_fmaf(-q1, b, a);
     return __builtin_fmaf(r1, y, q1);
 }
@@ -141,6 +149,14 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 // Every read is in bounds: the traversal stays within P of the grid, march()
 // returns before reading outside it, the AO sample clamps.
 constexpr uint32_t kSentinel = 0xFF00u;   // border cells hold 0xFFFF: size 255, colour 0xFF
+
+// Loads at a 32-bit byte offset from a wave-uniform base: lets the compiler
+// use the saddr form (SGPR base + VGPR offset) instead of 64-bit per-lane
+// address arithmetic.  Offsets here are < 2^31 (vx_scene_create limits).
+template <typename T>
+__device__ __forceinline__ T ld_off(const T *base, unsigned byte_off) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + byte_off);
+}
 
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
 __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
@@ -486,7 +502,7 @@ __device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1
     lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
-    auto ld = [&](int x, int y, int z) -> uint32_t { return (uint32_t)a.rg[lin_index(a, x, y, z)]; };
+    auto ld = [&](int x, int y, int z) -> uint32_t { return (uint32_t)ld_off(a.rg, lin_index(a, x, y, z) << 1); };
     const uint32_t t000 = ld(x0, y0, z0), t100 = ld(x1, y0, z0), t010 = ld(x0, y1, z0), t110 = ld(x1, y1, z0);
     const uint32_t t001 = ld(x0, y0, z1), t101 = ld(x1, y0, z1), t011 = ld(x0, y1, z1), t111 = ld(x1, y1, z1);
     float res[2];
@@ -521,10 +537,15 @@ __device__ float fbm(const KernelArgs &a, const float *unorm, float px, float py
     const float wa = u - fu, wb = v - fv;
     const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-    const float t00 = unorm[a.noise[(unsigned)y0 * W + x0] >> 24];
-    const float t10 = unorm[a.noise[(unsigned)y0 * W + x1] >> 24];
-    const float t01 = unorm[a.noise[(unsigned)y1 * W + x0] >> 24];
-    const float t11 = unorm[a.noise[(unsigned)y1 * W + x1] >> 24];
+    // A byte of texel (x, y): byte 4*(y*W + x) + 3, W = 2^noise_lw
+    auto ld = [&](int x, int y) -> uint32_t {
+        return (uint32_t)ld_off(reinterpret_cast<const uint8_t *>(a.noise),
+                                ((((unsigned)y << a.noise_lw) | (unsigned)x) << 2) + 3u);
+    };
+    const float t00 = unorm[ld(x0, y0)];
+    const float t10 = unorm[ld(x1, y0)];
+    const float t01 = unorm[ld(x0, y1)];
+    const float t11 = unorm[ld(x1, y1)];
     const float r0 = gmix(t00, t10, wa), r1 = gmix(t01, t11, wa);
     return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
@@ -598,8 +619,10 @@ __device__ void white(const KernelArgs &a, const float *unorm, float px, float p
     const float wa = u - fu, wb = v - fv;
     const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-    const uint32_t t00 = a.noise[(unsigned)y0 * W + x0], t10 = a.noise[(unsigned)y0 * W + x1];
-    const uint32_t t01 = a.noise[(unsigned)y1 * W + x0], t11 = a.noise[(unsigned)y1 * W + x1];
+    auto ld = [&](int x, int y) -> uint32_t {
+        return ld_off(a.noise, (((unsigned)y << a.noise_lw) | (unsigned)x) << 2);
+    };
+    const uint32_t t00 = ld(x0, y0), t10 = ld(x1, y0), t01 = ld(x0, y1), t11 = ld(x1, y1);
     float w[3];
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
