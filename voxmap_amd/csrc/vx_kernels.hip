@@ -443,7 +443,9 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
     } while (stop == 0 && ++it < cap);
     cnt.prim_witers += once_per_wave((unsigned)it + 1u);
     if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
-    asm volatile("" : "+v"(col));
+    // opaque after the loop: otherwise the compiler keeps the loop's compare
+    // masks (stop, tb == te) alive past it, at 3 SALU merges per mask per step
+    asm volatile("" : "+v"(col), "+v"(stop), "+v"(tb0), "+v"(tb1), "+v"(te));
     if (stop == 0) cnt.cap_hit++;
     const bool hit = stop != 0 && t < kSentinel;
     const int hax = tb0 == te ? 0 : (tb1 == te ? 1 : 2);    // exit axis of the last step (ties x < y < z)
@@ -878,29 +880,40 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
 #else
 #define VX_OCC_ATTR
 #endif
+// Workgroup = VX_WG threads: 256 (four 8x8-pixel waves, a 16x16 tile), 64
+// (one wave, an 8x8 tile) or 1024 (sixteen waves, a 32x32 tile).
+#ifndef VX_WG
+#define VX_WG 256
+#endif
+constexpr int kWG = VX_WG;
+constexpr int kBE = kWG == 1024 ? 32 : (kWG == 256 ? 16 : 8);   // block edge in pixels
+constexpr int kBS = kWG == 1024 ? 5 : (kWG == 256 ? 4 : 3);      // log2(kBE)
+constexpr int kWX = kBE / 8;                                       // waves per block row
 template <int FMT, bool STATS, bool TILED, bool EXT>
-__global__ __launch_bounds__(256) VX_OCC_ATTR
+__global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
     // unorm8 -> float table: b/255 as IEEE quotients (render.frag:38 decode)
     __shared__ float s_unorm[256];
-    s_unorm[threadIdx.x] = (float)threadIdx.x / 255.0f;
+#pragma unroll
+    for (int i = threadIdx.x; i < 256; i += kWG) s_unorm[i] = (float)i / 255.0f;
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int lx = ((wave & 1) << 3) | (lane & 7);
-    const int ly = ((wave >> 1) << 3) | (lane >> 3);
+    const int lx = ((wave % kWX) << 3) | (lane & 7);
+    const int ly = ((wave / kWX) << 3) | (lane >> 3);
     int ox, oy, tx0 = 0, ty0 = 0, tile_k = 0;
     if (TILED) {
-        const int bpt = (a.tile_size >> 4) * (a.tile_size >> 4);
+        const int per = a.tile_size >> kBS;
+        const int bpt = per * per;
         tile_k = blockIdx.x / bpt;
         const int sub = blockIdx.x % bpt;
         const int tid = a.tile_ids[tile_k];
-        tx0 = (sub % (a.tile_size >> 4)) << 4;
-        ty0 = (sub / (a.tile_size >> 4)) << 4;
+        tx0 = (sub % per) << kBS;
+        ty0 = (sub / per) << kBS;
         ox = (tid % a.tiles_x) * a.tile_size + tx0;
         oy = (tid / a.tiles_x) * a.tile_size + ty0;
     } else {
-        ox = blockIdx.x << 4;
-        oy = blockIdx.y << 4;
+        ox = blockIdx.x << kBS;
+        oy = blockIdx.y << kBS;
     }
     const int px = ox + lx, py = oy + ly;
     const FrameConsts &F = a.fc;
@@ -1044,8 +1057,9 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     const bool tiled = a.tile_ids != nullptr;
     const bool st = a.stats != nullptr;
-    dim3 block(256);
-    dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_size >> 4) * (a.tile_size >> 4)) : dim3((a.w + 15) / 16, (a.h + 15) / 16);
+    dim3 block(kWG);
+    dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_size >> kBS) * (a.tile_size >> kBS))
+                      : dim3((a.w + kBE - 1) / kBE, (a.h + kBE - 1) / kBE);
     const bool ext = (a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) || a.fc.n_sun > 1;
 #define VX_L(F, S, T, E) hipLaunchKernelGGL((k_render<F, S, T, E>), grid, block, 0, s, a)
 #define VX_LE(F, S, T) do { if (ext) VX_L(F, S, T, true); else VX_L(F, S, T, false); } while (0)
