@@ -23,6 +23,12 @@
 
 // Diagnostic padding (A/B only, never in the product build): VX_PAD_MARCH /
 // VX_PAD_PRIM extra independent v_add_f32 per loop iteration.
+#ifndef VX_RSTEP
+#define VX_RSTEP 1
+#endif
+#ifndef VX_STOP_VGPR
+#define VX_STOP_VGPR 1
+#endif
 #ifndef VX_MARCH_PAD
 #define VX_MARCH_PAD 1
 #endif
@@ -131,6 +137,14 @@ struct Counters {
     unsigned prim_witers, march_witers;      // loop iterations per wave (diagnostic: lane utilisation)
 };
 
+// (float)((t >> 8) & 0xff) as one v_cvt_f32_ubyte1 (the compiler folds the
+// mask away when it knows t < 2^16 and then emits a shift + convert)
+__device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
+    float r;
+    asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
 // v counted once per wave: by the first active lane (wave-uniform loop counts)
 __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
     const unsigned long long act = __ballot(1);
@@ -238,23 +252,36 @@ __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *
 // step (step MAX_STEPS-1 -> MAX_STEPS) is lit whatever it reads (:234), so
 // the loop runs MAX_STEPS-1 steps with the step test on the scalar unit, and
 // a lane still marching afterwards is lit.
-__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1, int c2, float f0,
-                          float f1, float f2, unsigned &fetches, unsigned &witers) {
+// rstep (hard shadows): an LDS table of (r0*k, r1*k, r2*k) for k = 0..127, the
+// same fp32 products r*safe of :118 for every possible safe, indexed by the
+// loaded texel -- one ds_read_b128 instead of three multiplies and the
+// byte -> float convert.  nullptr: multiply in the loop (soft-shadow samples).
+__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
+                                          int c2, float f0, float f1, float f2, unsigned &fetches, unsigned &witers,
+                                          const float4 *rstep) {
     const FrameConsts &F = a.fc;
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
     if (maxs <= 0) return maxs == 0;
     const float xpf = (float)a.SXp;
     float e0 = (float)(c0 + a.SB), e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB);
-    float safe = 1.0f;
     float len = march_len(S, f0, f1, f2);
     const unsigned sxpyp = a.SXpYp;
+    int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
     // one step of :94-128 -> the texel (-1: left the grid)
 #define VX_PAD_STEP(T)                                                                        \
     {                                                                                         \
-        f0 = f0 + (r0 * safe) * len; /* :118 */                                              \
-        f1 = f1 + (r1 * safe) * len;                                                          \
-        f2 = f2 + (r2 * safe) * len;                                                          \
+        float m0, m1, m2;                                                                     \
+        if (rstep) {                                                                          \
+            const float4 q = rstep[tv];                                                       \
+            m0 = q.x; m1 = q.y; m2 = q.z;                                                     \
+        } else {                                                                              \
+            const float safe = (float)tv;                                                     \
+            m0 = r0 * safe; m1 = r1 * safe; m2 = r2 * safe;                                   \
+        }                                                                                     \
+        f0 = f0 + m0 * len; /* :118 */                                                        \
+        f1 = f1 + m1 * len;                                                                   \
+        f2 = f2 + m2 * len;                                                                   \
         const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);                     \
         e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                                   \
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2; /* :120 */                               \
@@ -268,17 +295,17 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
             int t;
             VX_PAD_STEP(t)
             len = march_len(S, f0, f1, f2);                                      // next step, under the load
-            safe = (float)t;
-        } while (safe > 0.0f && ++step < maxs - 1);
+            tv = t;
+            witers += once_per_wave(1u);         // counted in the loop: step stays a scalar
+        } while (tv > 0 && ++step < maxs - 1);
     }
-    witers += once_per_wave((unsigned)step + 1u);
-    if (safe > 0.0f) {                         // the MAX_STEPS-th step: only its fetch (stats) matters
+    if (tv > 0) {                              // the MAX_STEPS-th step: only its fetch (stats) matters
         int t;
         VX_PAD_STEP(t)
         (void)t;
     }
 #undef VX_PAD_STEP
-    return safe != 0.0f;
+    return tv != 0;
 }
 
 // Literal path for any other sun direction (zero or tiny components: the
@@ -327,9 +354,11 @@ __device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_
 // reference into the kernel argument there made the compiler copy the whole
 // KernelArgs (1.5 KB) to scratch.
 __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
-                                          float f1, float f2, unsigned &fetches, unsigned &witers) {
+                                          float f1, float f2, unsigned &fetches, unsigned &witers,
+                                          const float4 *rstep = nullptr) {
     if (VX_MARCH_PAD && S.fast && a.sunp)
-        return march_pad(a, S, S.up ? a.sunp : a.sunp + a.sunp_texels, c0, c1, c2, f0, f1, f2, fetches, witers);
+        return march_pad(a, S, S.up ? a.sunp : a.sunp + a.sunp_texels, c0, c1, c2, f0, f1, f2, fetches, witers,
+                         VX_RSTEP ? rstep : nullptr);
     const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
     return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers)
                   : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers);
@@ -396,7 +425,7 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
     uint32_t t = fetch(h0, h1, h2);
     cnt.prim_fetch++;
     int prev = t & 0xff;
-    float R = (float)((t >> 8) & 0xffu);
+    float R = cvt_f32_ubyte1(t);
     // gmark: the colour whose entry is "the first glass" -- glass until a glass
     // entry is recorded, then 256 (matches nothing).  The sentinel's colour
     // byte 0xFF is no palette index (vx_scene_create), so leaving the grid is
@@ -437,11 +466,13 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
             gax = e0 ? 0 : (e1 ? 1 : 2);
         }
         stop = (change && !gfirst) ? 1 : 0;
+#if VX_STOP_VGPR
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
+#endif
         prev = col;
-        R = (float)((t >> 8) & 0xffu);
+        R = cvt_f32_ubyte1(t);
+        cnt.prim_witers += once_per_wave(1u);      // counted in the loop: it stays a scalar
     } while (stop == 0 && ++it < cap);
-    cnt.prim_witers += once_per_wave((unsigned)it + 1u);
     if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
     // opaque after the loop: otherwise the compiler keeps the loop's compare
     // masks (stop, tb == te) alive past it, at 3 SALU merges per mask per step
@@ -690,7 +721,8 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
         if (!EXT || F.n_sun <= 1) {
             cnt.shadow_rays++;
-            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch, cnt.march_witers);
+            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
+                                       cnt.march_witers, reinterpret_cast<const float4 *>(unorm + 256));
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
         } else {                       // ext soft shadows: lit fraction of the sun samples
             int lit = 0;
@@ -892,10 +924,17 @@ constexpr int kWX = kBE / 8;                                       // waves per 
 template <int FMT, bool STATS, bool TILED, bool EXT>
 __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
-    // unorm8 -> float table: b/255 as IEEE quotients (render.frag:38 decode)
-    __shared__ float s_unorm[256];
+    // LDS: [0, 256) unorm8 -> float table, b/255 as IEEE quotients (render.frag:38
+    // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
+    __shared__ float4 s_lds[64 + 128];
+    float *s_unorm = reinterpret_cast<float *>(s_lds);
 #pragma unroll
     for (int i = threadIdx.x; i < 256; i += kWG) s_unorm[i] = (float)i / 255.0f;
+    if (threadIdx.x < 128) {
+        const float k = (float)threadIdx.x;
+        const SunRay &S0 = a.fc.sun_k[0];
+        s_lds[64 + threadIdx.x] = make_float4(S0.r[0] * k, S0.r[1] * k, S0.r[2] * k, 0.0f);
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lx = ((wave % kWX) << 3) | (lane & 7);
