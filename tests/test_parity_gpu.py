@@ -127,13 +127,14 @@ def test_rgba8_is_quantised_rgba32f(full_scene):
     assert np.array_equal(u8, expect)
 
 
-def test_tiles_and_detile_equal_full_frame(full_scene):
+@pytest.mark.parametrize("flags,samples", [(0, 0), (0x30, 0), (0x30, 4)])
+def test_tiles_and_detile_equal_full_frame(full_scene, flags, samples):
     import torch
     import voxmap_amd as vx
     from voxmap_amd import presets
     sc, _ = full_scene
     w, h, ts = 1000, 600, 64            # ragged: w, h not multiples of the tile
-    fr = presets.camera_frame("K1", w, h)
+    fr = presets.camera_frame("K1", w, h, flags=flags, shadow_samples=samples, sun_radius=0.03)
     full, _ = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
     tx, ty = -(-w // ts), -(-h // ts)
     ids = list(range(tx * ty))[::-1]    # any order
