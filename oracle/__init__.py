@@ -85,13 +85,18 @@ def lib():
 class Oracle:
     """Scalar restatement of render.frag over one field + noise texture."""
 
-    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32):
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_r=None):
         self.field = np.ascontiguousarray(field_zyx4, np.uint8)
         self.noise = np.ascontiguousarray(noise_hw4, np.uint8)
         Z, Y, X, _ = self.field.shape
         H, W, _ = self.noise.shape
-        # the primary traversal's octant cubes (vxo_field_octant), from the colours
-        self.oct_r = [field_octant(self.field, o, cap) for o in range(8)]
+        # the primary traversal's octant cubes (vxo_field_octant), from the colours;
+        # oct_r: precomputed (Z, Y, X) arrays (e.g. device copies checked elsewhere
+        # against field_octant) for fields too large for the scalar pass
+        if oct_r is None:
+            self.oct_r = [field_octant(self.field, o, cap) for o in range(8)]
+        else:
+            self.oct_r = [np.ascontiguousarray(r, np.uint8) for r in oct_r]
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
                          (C.c_void_p * 8)(*[r.ctypes.data for r in self.oct_r]))
 

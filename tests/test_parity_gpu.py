@@ -284,3 +284,30 @@ def test_scene_from_grid_equals_scene_from_field(noise):
         ia, _ = a.render(fr)
         ib, _ = b.render(fr)
     assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32))
+
+
+def test_c5_rows_soft_shadows_full_quality(noise):
+    """BASELINE C5: 3^3-upscaled 3072x768x96 field, 3840x2160, 16-sample soft
+    shadows + full quality, on a deterministic row subset.  The oracle takes the
+    device's octant-cube copies (checked against vxo_field_octant at smaller
+    sizes above) -- its scalar octant pass over 226 M cells would take hours."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid("s_up3")
+    Z, Y, X = grid.shape
+    c = presets.CONFIGS["C5"]
+    fr = presets.camera_frame("K1", c["w"], c["h"], scale=3.0, flags=vx.FLAG_FULL_QUALITY, shadow_samples=16,
+                              sun_radius=0.03)
+    with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
+        img, st = sc.render(fr, stats=True)
+        field = sc.read_field(0)
+        oct_r = [np.ascontiguousarray(field[..., 3])] + [np.ascontiguousarray(sc.read_field(o)[..., 3])
+                                                        for o in range(1, 8)]
+    step = 271
+    ref, _ = oracle.Oracle(field, noise, oct_r=oct_r).render(fr.params, c["w"], c["h"], row0=step // 2,
+                                                            row_step=step, threads=16)
+    rows = np.arange(step // 2, c["h"], step)
+    _compare(img, ref, rows)
+    assert st.primary_cap_hits == 0

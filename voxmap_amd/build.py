@@ -29,6 +29,19 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+CLI = os.path.join(HERE, "vxrender")
+
+
+def build_cli(verbose: bool = False) -> str:
+    """The C++ host (csrc/vx_cli.cpp) over the C ABI, linked to the in-tree library."""
+    cmd = [hipcc(), "-O2", "-std=c++20", f"--offload-arch={ARCH}", "-o", CLI, os.path.join(CSRC, "vx_cli.cpp"),
+           f"-L{HERE}", "-lvoxmap_hip", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return CLI
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
@@ -51,6 +64,8 @@ def build(force: bool = False, verbose: bool = True, out: str | None = None, def
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, target)
+    if out is None:
+        build_cli(verbose)
     return target
 
 
