@@ -37,8 +37,11 @@ TILE = 64
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed frames rendered before the warmup so the GPU clock leaves its idle state "
+                         "(a ~5 ms burst runs ~12%% slower than steady state: profiles/r01_clock_settle.txt)")
     ap.add_argument("--config", default="C3")
     ap.add_argument("--camera", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
@@ -124,6 +127,23 @@ def main():
         stats = {k: float(v) for k, v in zip(keys, vec.tolist())}
         stats["kernel_ms"] = float(st.kernel_ms)
 
+    # clock settle: every rank renders the same number of untimed frames (the
+    # sharded step holds a collective), sized from a short probe to ~settle_ms
+    settle_steps = 0
+    if args.settle_ms > 0:
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        probe_ms = 1000.0 * (time.perf_counter() - tp) / 3
+        n = torch.tensor([math.ceil(args.settle_ms / max(probe_ms, 1e-3))], dtype=torch.int64,
+                         device="cuda" if world > 1 else "cpu")
+        if world > 1:
+            dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        settle_steps = int(min(int(n.item()), 20000)) + 3
+        for _ in range(settle_steps - 3):
+            step()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -212,6 +232,7 @@ def main():
                     (f" + {samples}-sample soft shadows (sun radius {args.sun_radius})" if samples > 1 else "") +
                     f", field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, RGBA8 framebuffer in HBM",
                 "flags": flags, "shadow_samples": samples, "scene_build_s": round(t_scene, 3),
+                "clock_settle": {"ms": args.settle_ms, "untimed_frames": settle_steps},
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
                 "tiles": {"size": TILE, "count": n_tiles, "assignment": "round-robin"} if world > 1 else None,
                 "fps": round(1000.0 / ms_per_step, 2),

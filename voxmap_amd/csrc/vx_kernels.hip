@@ -583,9 +583,26 @@ __device__ float fbm(const KernelArgs &a, const float *unorm, float px, float py
     return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
 
+// a / b for any sign of a (b > 0, y = RN(1/b)): div_const with the sign of a
+// copied onto the result, so a = -0 gives -0 as the IEEE quotient does.
+// One correction is exact for every pair of significands
+// (tools/micro/markstein_all.hip, profiles/r01_markstein_all.txt), so the
+// divisor may vary per pixel.
+__device__ __forceinline__ float div_shared(float a, float b, float y) {
+    return __builtin_copysignf(div_const(a, b, y), a);
+}
+
+#ifndef VX_NORM_MK
+#define VX_NORM_MK 1
+#endif
 __device__ __forceinline__ void normalize3(float v0, float v1, float v2, float &o0, float &o1, float &o2) {
     const float l = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
-    o0 = v0 / l; o1 = v1 / l; o2 = v2 / l;
+    if (VX_NORM_MK) {               // one IEEE reciprocal, three exact corrections
+        const float y = 1.0f / l;
+        o0 = div_shared(v0, l, y); o1 = div_shared(v1, l, y); o2 = div_shared(v2, l, y);
+    } else {
+        o0 = v0 / l; o1 = v1 / l; o2 = v2 / l;
+    }
 }
 
 // ---------------- render.frag main(), sky branch (render.frag:148-205) ----------------
@@ -616,7 +633,13 @@ __device__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, flo
     cnt.noise_px++;
     const float ct = F.cloudTime;
     const float den = sqrtf(fabsf(r2) + 0.03f);
-    float sx = r0 / den, sy = r1 / den;                                           // :184
+    float sx, sy;                                                                 // :184
+    if (VX_NORM_MK) {
+        const float y = 1.0f / den;
+        sx = div_shared(r0, den, y); sy = div_shared(r1, den, y);
+    } else {
+        sx = r0 / den; sy = r1 / den;
+    }
     sx = sx * 0.1f; sy = sy * 0.1f;
     const float sl = sqrtf(sqrtf(sx * sx + sy * sy));
     sx = sx * sl; sy = sy * sl;
@@ -852,14 +875,6 @@ __device__ void reflect_color(const KernelArgs &a, const float *unorm, const Sur
         shade_sky(a, unorm, R0, R1, R2, rgba, cnt);
     out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
 }
-
-// =====================================================================
-// Two pixels per lane (PAIR): each lane steps two independent rays back to
-// back, so the dependent texel-load -> ALU chains of both overlap (ILP 2).
-// The kernel is latency-bound at the 8-waves/SIMD maximum (halving the waves
-// costs 1.46x), so a second independent chain per wave is the lever.
-// Same arithmetic, same results as the one-pixel path.
-// =====================================================================
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     unsigned long long s = v;
