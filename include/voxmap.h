@@ -60,6 +60,9 @@ extern "C" {
 #define VX_FLAG_REFLECT 0x10u    /* glass mirrors the traced scene (Fresnel-weighted) */
 #define VX_FLAG_ROUGH 0x20u      /* shading normal jittered by white() noise (render.frag:21) */
 #define VX_FLAG_FULL_QUALITY (VX_FLAG_REFLECT | VX_FLAG_ROUGH)
+/* Diagnostics: force the integer primary-index path (the fp32 one is chosen
+ * whenever it is exact; both give identical frames). */
+#define VX_FLAG_INT_INDEX 0x40u
 #define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;

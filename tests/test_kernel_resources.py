@@ -1,0 +1,36 @@
+"""The built render kernels keep their occupancy and carry no KernelArgs copy
+in scratch (voxmap_amd/kernel_meta.py).  CPU only: reads the
+gfx950 code object's metadata out of the in-tree library."""
+import pytest
+
+
+@pytest.fixture(scope="module")
+def meta(built):
+    from voxmap_amd import build as vb
+    from voxmap_amd import kernel_meta
+    return kernel_meta.check(vb.OUT)
+
+
+def _render(meta):
+    from voxmap_amd import kernel_meta
+    return {kernel_meta.render_params(k): v for k, v in meta.items() if kernel_meta.render_params(k)}
+
+
+def test_every_render_instantiation_present(meta):
+    # FMT 2 x STATS 2 x TILED 2 x EXT mode 3 x primary index 2
+    assert len(_render(meta)) == 48
+
+
+def test_render_kernels_fit_eight_waves_and_no_arg_copy(meta):
+    from voxmap_amd import kernel_meta
+    for p, v in _render(meta).items():
+        assert v["private_segment_fixed_size"] <= kernel_meta.RENDER_SCRATCH_LIMIT, (p, v)
+        if not p[1]:                                   # timed (non-STATS) kernels
+            assert v["vgpr_count"] <= 64 and v["sgpr_count"] <= 80, (p, v)
+
+
+def test_v1_kernel_has_no_spills(meta):
+    """The reference shader's instantiations (EXT 0, not STATS) run spill-free."""
+    v1 = [v for p, v in _render(meta).items() if p[3] == 0 and p[1] == 0]
+    assert len(v1) == 8
+    assert all(v["vgpr_spill_count"] == 0 and v["private_segment_fixed_size"] == 0 for v in v1)

@@ -127,6 +127,23 @@ def test_rgba8_is_quantised_rgba32f(full_scene):
     assert np.array_equal(u8, expect)
 
 
+@pytest.mark.parametrize("cam", ["K0", "K1", "K2"])
+@pytest.mark.parametrize("flags,samples", [(0, 0), (0x30, 0), (0x30, 4)])
+def test_fp32_and_integer_primary_index_agree(full_scene, cam, flags, samples):
+    """The fp32 x/y primary index (chosen by vx_render where exact, as on this
+    field) and the integer one (VX_FLAG_INT_INDEX) give the same frame and
+    counters; the oracle rows above pin the fp32 path, the C5 rows (6.7 GB of
+    copies: integer path) the other."""
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    sc, _ = full_scene
+    kw = dict(shadow_samples=samples, sun_radius=0.03 if samples > 1 else 0.0)
+    a, sa = sc.render(presets.camera_frame(cam, 960, 540, flags=flags, **kw), stats=True)
+    b, sb = sc.render(presets.camera_frame(cam, 960, 540, flags=flags | vx.FLAG_INT_INDEX, **kw), stats=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa.as_dict() | {"kernel_ms": 0} == sb.as_dict() | {"kernel_ms": 0}
+
+
 @pytest.mark.parametrize("flags,samples", [(0, 0), (0x30, 0), (0x30, 4)])
 def test_tiles_and_detile_equal_full_frame(full_scene, flags, samples):
     import torch

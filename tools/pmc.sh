@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for set in "$@"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
+  timeout -s KILL 90 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
       python3 "$ROOT/bench.py" $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($set) failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
 echo "pmc passes done"

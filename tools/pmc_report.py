@@ -6,7 +6,7 @@ import sys
 from collections import defaultdict
 
 src = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "k_render<1, false, false>"
+kern = sys.argv[2] if len(sys.argv) > 2 else "k_render<1, false, false,"
 vals = defaultdict(list)
 for f in sorted(glob.glob(f"{src}/p*/run_counter_collection.csv")):
     for row in csv.DictReader(open(f)):

@@ -23,7 +23,9 @@ cam = sys.argv[4] if len(sys.argv) > 4 else "K1"
 flags = int(sys.argv[5]) if len(sys.argv) > 5 else 48          # VX_FLAG_FULL_QUALITY
 samples = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 # the bench's timed kernel: RGBA8, no stats, untiled; EXT instantiation unless v1
-KERNEL = f"k_render<1, false, false, {'true' if (flags & 0x30) or samples > 1 else 'false'}>"
+# EXT mode 0 v1 / 1 extensions / 2 soft shadows; either primary-index
+# instantiation (the last template argument is left open)
+KERNEL = f"k_render<1, false, false, {2 if samples > 1 else (1 if flags & 0x30 else 0)},"
 os.makedirs("profiles", exist_ok=True)
 shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"profiles/{tag}_kernel_stats.csv")
 

@@ -26,6 +26,7 @@ PIXEL_RGBA32F, PIXEL_RGBA8 = 0, 1
 FLAG_NO_SHADOW, FLAG_NO_AO, FLAG_NO_CLOUDS, FLAG_PRIMARY_ONLY = 0x1, 0x2, 0x4, 0x8
 FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
 FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
+FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary index path
 MAX_SHADOW_SAMPLES = 16
 ABI_VERSION = 2
 

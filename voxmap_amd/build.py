@@ -63,6 +63,14 @@ def build(force: bool = False, verbose: bool = True, out: str | None = None, def
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    if not defines and not extra_flags:
+        # the product must keep 8 waves/SIMD and no KernelArgs scratch copy
+        from . import kernel_meta
+        try:
+            kernel_meta.check(tmp)
+        except Exception:
+            os.remove(tmp)
+            raise
     os.replace(tmp, target)
     if out is None:
         build_cli(verbose)

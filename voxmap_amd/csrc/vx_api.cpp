@@ -347,6 +347,19 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.copy_texels = (unsigned)s->L.texels;
     a.kcam = (unsigned)(p->cam_cell[0] + s->L.pad) + (unsigned)a.Xp * (unsigned)(p->cam_cell[1] + s->L.pad) +
              a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);   // mod 2^32
+    {
+        // fp32 x/y index: 2*(x + Xp*y) of a fetched cell lies in [0, 2*Xp*Yp),
+        // its partial sums 2x in [0, 2Xp) and y in [0, Yp), all exact fp32
+        // integers below 2^24; the 24-bit multiply needs 2*Xp*Yp < 2^23, the
+        // 32-bit byte offsets all 8 copies below 4 GiB
+        const double xy2 = 2.0 * (double)s->L.Xp * (double)s->L.Yp;
+        const bool ok = xy2 < 8388608.0 && 16.0 * (double)s->L.texels < 4294967296.0 &&
+                        std::abs(p->cam_cell[0]) < (1 << 21) && std::abs(p->cam_cell[1]) < (1 << 21);
+        a.prim_f32 = ok && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
+        a.kx2 = (float)(2 * (p->cam_cell[0] + s->L.pad));
+        a.ky = (float)(p->cam_cell[1] + s->L.pad);
+        a.kz = 2u * a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);
+    }
 
     if (stats) {
         a.stats = s->d_stats;

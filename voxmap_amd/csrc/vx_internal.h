@@ -78,6 +78,12 @@ struct KernelArgs {
     unsigned copy_texels;    // cells per prim copy (FieldLayout::texels)
     unsigned kcam;           // padded index of the camera cell, mod 2^32
     FrameConsts fc;
+    // fp32 x/y primary index (vx_render decides): byte offset
+    // from prim = cvt(fma(2Xp, h1 + ky, fma(2, h0, kx2))) + 2XpYp*(int)h2 + kz2
+    // (mod 2^32), exact while 2*Xp*Yp < 2^23 and the 8 copies < 4 GiB
+    int prim_f32;            // 0: the integer index path
+    float kx2, ky;           // 2*(camera padded x), camera padded y (ray octant terms added per lane)
+    unsigned kz;             // 2*XpYp*(camera padded z), mod 2^32
 };
 
 void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, int max_steps, FrameConsts &fc);

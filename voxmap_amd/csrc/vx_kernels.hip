@@ -384,7 +384,8 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, i
 // axis, [h - R, h] on a negative one, i.e. [fma(hp - 1, R, h), fma(hp, R, h)].
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, float d1, float d2, Surf &g0, Surf &g1,
+template <bool F32IDX>
+__device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d2, Surf &g0, Surf &g1,
                        Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
@@ -417,8 +418,21 @@ __device__ int primary(const KernelArgs &a, const uint16_t *ppad, float d0, floa
     float h0 = (float)(c0 + ip0), h1 = (float)(c1 + ip1), h2 = (float)(c2 + ip2);
     // padded index of h: kray + hx + Xp*hy + XpYp*hz, mod 2^32 with 24-bit
     // signed products (|h| < 2^23)
+    const uint16_t *ppad = a.prim + (size_t)oct * a.copy_texels;
     const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
+    // F32IDX (a.prim_f32): 2*(x + Xp*y) in fp32 (exact, < 2^23), z by a
+    // 24-bit multiply-add, a 32-bit byte offset from a.prim: 2 fma + add +
+    // 2 cvt + mad24 + add instead of 3 cvt + 2 mul24 + add3 + a 64-bit add
+    const float kx2 = a.kx2 - (float)(2 * ip0), ky = a.ky - (float)ip1;
+    const float fXp2 = (float)(2 * a.Xp);
+    const int XpYp2 = (int)(2u * a.XpYp);
+    const unsigned kz = a.kz - (unsigned)XpYp2 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 1);
     auto fetch = [&](float x, float y, float z) -> uint32_t {
+        if (F32IDX) {
+            const float xy = __builtin_fmaf(fXp2, y + ky, __builtin_fmaf(2.0f, x, kx2));
+            const unsigned off = (unsigned)(int)xy + ((unsigned)__mul24(XpYp2, (int)z) + kz);
+            return (uint32_t)ld_off(a.prim, off);
+        }
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
         return (uint32_t)ppad[(unsigned)idx];
     };
@@ -697,7 +711,7 @@ constexpr float kRoughAmp = 0.1f;
 // EXT: the extension instantiation (rough normals, soft shadows); has_ray:
 // rayDir is given (a surface seen in a reflection) instead of the camera ray
 // to the fragment (:154).  ray_out receives the rayDir used.
-template <bool EXT>
+template <int EXT>
 __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt,
                             bool has_ray = false, float q0 = 0.0f, float q1 = 0.0f, float q2 = 0.0f,
                             float *ray_out = nullptr) {
@@ -742,12 +756,12 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
     if (rough)
         shadeFactor = F.sun[2] < 0.0f ? 0.0f : sqrtf(gmax(0.0f, (m0 * F.sun[0] + m1 * F.sun[1]) + m2 * F.sun[2]));
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
-        if (!EXT || F.n_sun <= 1) {
+        if (EXT != 2) {                // the reference's hard shadow: one sun ray
             cnt.shadow_rays++;
             const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
                                        cnt.march_witers, reinterpret_cast<const float4 *>(unorm + 256));
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
-        } else {                       // ext soft shadows: lit fraction of the sun samples
+        } else {                       // ext soft shadows (EXT == 2): lit fraction of the sun samples
             int lit = 0;
             for (int k = 0; k < F.n_sun; k++) {
                 cnt.shadow_rays++;
@@ -852,6 +866,7 @@ __device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o
 // ext REFLECT: colour seen along the mirror reflection at glass record gl
 // (rd = the camera rayDir at the fragment; R = rd with the face-axis
 // component negated = reflect(rd, n) exactly), oracle reflect_color().
+template <int EXT>
 __device__ void reflect_color(const KernelArgs &a, const float *unorm, const Surf &gl, const float rd[3], float out[3],
                               Counters &cnt) {
     const int ax = gl.nidx >> 1;
@@ -870,7 +885,7 @@ __device__ void reflect_color(const KernelArgs &a, const float *unorm, const Sur
     Surf h;
     float rgba[4];
     if (walk_reflect(a, B0, B1, B2, o0, o1, o2, R0, R1, R2, s0, s1, s2, h, cnt))
-        shade_block<true>(a, unorm, h, rgba, cnt, true, R0, R1, R2);
+        shade_block<EXT>(a, unorm, h, rgba, cnt, true, R0, R1, R2);
     else
         shade_sky(a, unorm, R0, R1, R2, rgba, cnt);
     out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
@@ -913,8 +928,11 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
 }
 
 // Lane = pixel, wave = 8x8 tile, workgroup = 16x16 pixels.
-// EXT: the extension instantiation (REFLECT, ROUGH, soft shadows); the v1
-// instantiation does not carry their registers or code.
+// EXT: 0 = v1 (the reference's shader), 1 = extensions (REFLECT, ROUGH) with
+// the hard shadow, 2 = extensions with soft shadows (n sun samples).  Each
+// instantiation carries only its own code and registers; soft shadows in a
+// kernel of their own also keep the sun_k[0] / sun_k[k] addresses apart (a
+// pointer phi between them makes the compiler copy KernelArgs to scratch).
 // Occupancy: 8 waves/SIMD needs <= 64 VGPRs and <= 80 SGPRs (8 256-thread
 // blocks per CU, MI355X_MICROARCH.md "Residency"); the EXT instantiation is
 // held to that budget explicitly (left alone it takes 66 VGPRs + 100 SGPRs
@@ -936,10 +954,15 @@ constexpr int kWG = VX_WG;
 constexpr int kBE = kWG == 1024 ? 32 : (kWG == 256 ? 16 : 8);   // block edge in pixels
 constexpr int kBS = kWG == 1024 ? 5 : (kWG == 256 ? 4 : 3);      // log2(kBE)
 constexpr int kWX = kBE / 8;                                       // waves per block row
-template <int FMT, bool STATS, bool TILED, bool EXT>
+
+// F32IDX: the fp32 primary index (a.prim_f32) -- a kernel of its own: two
+// inlined primary() copies in one kernel make the compiler copy KernelArgs
+// to scratch.
+template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
 __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
     // LDS: [0, 256) unorm8 -> float table, b/255 as IEEE quotients (render.frag:38
+    // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     __shared__ float4 s_lds[64 + 128];
     float *s_unorm = reinterpret_cast<float *>(s_lds);
@@ -979,7 +1002,7 @@ void k_render(KernelArgs a) {
         // the field copy of this ray's octant (zero components count positive)
         const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
         Surf g[2];
-        const int n = primary(a, a.prim + (size_t)oct * a.copy_texels, d0, d1, d2, g[0], g[1], cnt);
+        const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt);
         float rgba[4];
         if (F.flags & VX_FLAG_PRIMARY_ONLY) {
             primary_only_colour(n, g[0], rgba);
@@ -997,7 +1020,7 @@ void k_render(KernelArgs a) {
                 if (EXT && (F.flags & VX_FLAG_REFLECT)) {
                     // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
                     float refl[3];
-                    reflect_color(a, s_unorm, g[0], rd, refl, cnt);
+                    reflect_color<EXT>(a, s_unorm, g[0], rd, refl, cnt);
                     const int ax = g[0].nidx >> 1;
                     const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
                     const float x = 1.0f - cs, x2 = x * x;
@@ -1107,6 +1130,14 @@ __global__ void k_reduce_stats(unsigned long long *stats) {
 
 }  // namespace
 
+template <int F, bool S, bool T, int E>
+static void launch_k(const KernelArgs &a, dim3 grid, dim3 block, hipStream_t s) {
+    if (a.prim_f32)
+        hipLaunchKernelGGL((k_render<F, S, T, E, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, block, 0, s, a);
+}
+
 int launch_render(const KernelArgs &a, int fmt, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     const bool tiled = a.tile_ids != nullptr;
@@ -1114,9 +1145,9 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
     dim3 block(kWG);
     dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_size >> kBS) * (a.tile_size >> kBS))
                       : dim3((a.w + kBE - 1) / kBE, (a.h + kBE - 1) / kBE);
-    const bool ext = (a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) || a.fc.n_sun > 1;
-#define VX_L(F, S, T, E) hipLaunchKernelGGL((k_render<F, S, T, E>), grid, block, 0, s, a)
-#define VX_LE(F, S, T) do { if (ext) VX_L(F, S, T, true); else VX_L(F, S, T, false); } while (0)
+    const int ext = a.fc.n_sun > 1 ? 2 : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
+#define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
+#define VX_LE(F, S, T) do { if (ext == 2) VX_L(F, S, T, 2); else if (ext) VX_L(F, S, T, 1); else VX_L(F, S, T, 0); } while (0)
 #define VX_LT(F, S) do { if (tiled) VX_LE(F, S, true); else VX_LE(F, S, false); } while (0)
     if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_LT(0, true); else VX_LT(0, false); }
     else { if (st) VX_LT(1, true); else VX_LT(1, false); }

@@ -1,0 +1,95 @@
+"""Per-kernel resource metadata of a built library (scratch, registers, spills).
+
+Reads the gfx950 code object out of the library's ``.hip_fatbin`` section
+(``llvm-objcopy`` + ``clang-offload-bundler``) and parses its AMDHSA metadata
+note (``llvm-readelf --notes``).  ``check()`` is the guard ``build()`` runs:
+the render kernels must keep 8 waves/SIMD (<= 64 VGPRs) and must not carry a
+KernelArgs-sized private segment -- a pointer phi into the kernel arguments
+makes the compiler copy the whole 1.7 KB struct to scratch per thread, which
+fails silently (correct frames, ~14 GB of scratch traffic per frame).
+DESIGN.md §3 lists the measured budgets.
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+FIELDS = ("private_segment_fixed_size", "vgpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
+          "group_segment_fixed_size")
+RENDER_SCRATCH_LIMIT = 256      # bytes per thread: spill slots yes, a KernelArgs copy (~1.7 KB) no
+RENDER_VGPR_LIMIT = 64          # 8 waves/SIMD
+
+
+def _tool(name: str) -> str:
+    p = os.path.join(LLVM, name)
+    return p if os.path.exists(p) else name
+
+
+def kernels(lib: str) -> dict[str, dict[str, int]]:
+    """{mangled kernel name: {field: value}} for every kernel in ``lib``."""
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        subprocess.run([_tool("llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", lib, os.path.join(d, "x")],
+                       check=True, capture_output=True)
+        subprocess.run([_tool("clang-offload-bundler"), "--unbundle", "--type=o", f"--targets={TARGET}",
+                        f"--input={fb}", f"--output={co}"], check=True, capture_output=True)
+        notes = subprocess.run([_tool("llvm-readelf"), "--notes", co], check=True, capture_output=True,
+                               text=True).stdout
+    # one YAML list item per kernel ("- .agpr_count: ..."), keys in alphabetical
+    # order, so .group_segment_fixed_size precedes .name within the item
+    out: dict[str, dict[str, int]] = {}
+    blocks, cur = [], None
+    for line in notes.splitlines():
+        if re.match(r"\s+- \.", line):
+            cur = {}
+            blocks.append(cur)
+        if cur is None:
+            continue
+        m = re.match(r"\s+(?:- )?\.name:\s+(\S+)$", line)
+        if m:
+            cur["__name"] = m.group(1)
+            continue
+        m = re.match(r"\s+(?:- )?\.(\w+):\s+(\d+)$", line)
+        if m and m.group(1) in FIELDS:
+            cur[m.group(1)] = int(m.group(2))
+    for b in blocks:
+        name = b.pop("__name", None)
+        if name and "private_segment_fixed_size" in b:
+            out[name] = b
+    return out
+
+
+def render_params(name: str):
+    """(FMT, STATS, TILED, EXT, F32IDX) of a mangled k_render instantiation, else None."""
+    m = re.search(r"k_renderILi(\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)E", name)
+    return tuple(int(g) for g in m.groups()) if m else None
+
+
+def check(lib: str) -> dict[str, dict[str, int]]:
+    """Raise if a render kernel copies its arguments to scratch or loses occupancy."""
+    ks = kernels(lib)
+    render = {k: v for k, v in ks.items() if "k_render" in k}
+    if not render:
+        raise RuntimeError(f"{lib}: no k_render kernels found in the gfx950 code object")
+    bad = []
+    for name, v in render.items():
+        p = render_params(name)
+        stats = p is not None and p[1] == 1                        # STATS instantiation: counting only
+        if v.get("private_segment_fixed_size", 0) > RENDER_SCRATCH_LIMIT:
+            bad.append(f"{name}: private segment {v['private_segment_fixed_size']} B > {RENDER_SCRATCH_LIMIT}")
+        if not stats and v.get("vgpr_count", 0) > RENDER_VGPR_LIMIT:
+            bad.append(f"{name}: {v['vgpr_count']} VGPRs > {RENDER_VGPR_LIMIT}")
+    if bad:
+        raise RuntimeError("render kernel resource check failed:\n  " + "\n  ".join(bad))
+    return ks
+
+
+if __name__ == "__main__":
+    import sys
+    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "libvoxmap_hip.so")
+    for name, v in sorted(kernels(lib).items()):
+        print(f"{name[:70]:70s} " + " ".join(f"{f.split('_')[0][:5]}={v.get(f, 0)}" for f in FIELDS))
