@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 2
+#define VX_ABI_VERSION 3
 
 /* error codes */
 #define VX_OK 0
@@ -130,11 +130,15 @@ typedef struct vx_stats {
 int vx_scene_create(const vx_scene_desc *desc, vx_scene **out);
 void vx_scene_destroy(vx_scene *scene);
 /* Copy the device-resident field back (RGBA8 X*Y*Z, x fastest).  The device
- * keeps one copy per ray octant (bit 0/1/2: x/y/z direction negative) whose A
- * byte is that octant's air-cube size for the primary traversal (DESIGN.md
- * §3); R, G, B are map.bin's.  vx_scene_read_field reads octant 0. */
+ * keeps one copy per ray octant (bit 0/1/2: x/y/z direction negative) holding
+ * the colour and the extents of the all-air box ahead of each cell for the
+ * primary traversal.  vx_scene_read_field[_copy]: R, G, B are
+ * map.bin's, A is the octant's air-cube size (= the smallest box extent);
+ * vx_scene_read_field reads octant 0.  vx_scene_read_boxes: 4 bytes per cell,
+ * colour, ex, ey, ez (ABI 3). */
 int vx_scene_read_field(vx_scene *scene, void *host_out, size_t cap);
 int vx_scene_read_field_copy(vx_scene *scene, int octant, void *host_out, size_t cap);
+int vx_scene_read_boxes(vx_scene *scene, int octant, void *host_out, size_t cap);
 int vx_scene_dims(const vx_scene *scene, int dims[3]);
 
 /* --- rendering (replaces gl.drawArrays at render.js:297 + the shaders) --- */

@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(_HERE, "build", "libvxo.so")
 
 class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
-                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_r", C.c_void_p * 8)]
+                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8)]
 
 
 class OStats(C.Structure):
@@ -78,6 +78,7 @@ def lib():
         L.vxo_exp2.restype = C.c_float
         L.vxo_field_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vxo_field_octant.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.vxo_field_box.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -85,20 +86,22 @@ def lib():
 class Oracle:
     """Scalar restatement of render.frag over one field + noise texture."""
 
-    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_r=None):
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_e=None):
         self.field = np.ascontiguousarray(field_zyx4, np.uint8)
         self.noise = np.ascontiguousarray(noise_hw4, np.uint8)
         Z, Y, X, _ = self.field.shape
         H, W, _ = self.noise.shape
-        # the primary traversal's octant cubes (vxo_field_octant), from the colours;
-        # oct_r: precomputed (Z, Y, X) arrays (e.g. device copies checked elsewhere
-        # against field_octant) for fields too large for the scalar pass
-        if oct_r is None:
-            self.oct_r = [field_octant(self.field, o, cap) for o in range(8)]
+        # the primary traversal's octant boxes (vxo_field_box), from the colours;
+        # oct_e: precomputed (Z, Y, X, 3) arrays (e.g. device copies checked
+        # elsewhere against field_box) for fields too large for the scalar pass
+        if oct_e is None:
+            self.oct_e = [field_box(self.field, o, cap) for o in range(8)]
         else:
-            self.oct_r = [np.ascontiguousarray(r, np.uint8) for r in oct_r]
+            self.oct_e = [np.ascontiguousarray(e, np.uint8) for e in oct_e]
+        for e in self.oct_e:
+            assert e.shape == (Z, Y, X, 3)
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
-                         (C.c_void_p * 8)(*[r.ctypes.data for r in self.oct_r]))
+                         (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]))
 
     def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
         """RGBA fp32 (h, w, 4); rows not in (row0::row_step) are NaN."""
@@ -148,6 +151,17 @@ def field_octant(field_zyx4: np.ndarray, oct: int, cap: int = 32) -> np.ndarray:
     Z, Y, X, _ = f.shape
     out = np.empty((Z, Y, X), np.uint8)
     lib().vxo_field_octant(f.ctypes.data, X, Y, Z, cap, oct, out.ctypes.data)
+    return out
+
+
+def field_box(field_zyx4: np.ndarray, oct: int, cap: int = 32, r_cube=None) -> np.ndarray:
+    """(Z, Y, X, 3) uint8: extents (ex, ey, ez) of the all-air box ahead of each
+    cell for ray octant ``oct`` (vxo_field_box, grown from field_octant)."""
+    f = np.ascontiguousarray(field_zyx4, np.uint8)
+    Z, Y, X, _ = f.shape
+    r = np.ascontiguousarray(field_octant(f, oct, cap) if r_cube is None else r_cube, np.uint8)
+    out = np.empty((Z, Y, X, 3), np.uint8)
+    lib().vxo_field_box(f.ctypes.data, X, Y, Z, cap, oct, r.ctypes.data, out.ctypes.data)
     return out
 
 

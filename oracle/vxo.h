@@ -36,7 +36,7 @@ typedef struct {
     const uint8_t *field;     /* RGBA8 X*Y*Z texels, x fastest (render.js:62) */
     const uint8_t *noise;     /* RGBA8 noise texture (render.js:138-149) */
     int noise_w, noise_h;
-    const uint8_t *oct_r[8];  /* vxo_field_octant per ray octant (primary traversal) */
+    const uint8_t *oct_e[8];  /* vxo_field_box per ray octant: 3 extents per cell (primary traversal) */
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */
@@ -133,6 +133,12 @@ void vxo_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba);
  * (bit 0/1/2: x/y/z direction negative), capped: the primary traversal's own
  * data, X*Y*Z bytes into r_out. */
 void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, uint8_t *r_out);
+/* Per-cell extents (ex, ey, ez) of the all-air box [c, c + e*s] the primary
+ * traversal jumps across: grown from the cube r (r_cube, from
+ * vxo_field_octant) to the largest x extent, then y, then z, each <= cap - 1;
+ * (0, 0, 0) for non-air cells.  3*X*Y*Z bytes into e_out, x fastest. */
+void vxo_field_box(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, const uint8_t *r_cube,
+                   uint8_t *e_out);
 
 #ifdef __cplusplus
 }

@@ -20,7 +20,7 @@
  * vxo_field_octant: the build's own primary-traversal data:
  * per octant of ray directions, the size r of the all-air cube ahead of each
  * cell (r <= cap - 1 <= 254; the kernels keep 255 for their out-of-grid
- * sentinel).
+ * sentinel).  vxo_field_box grows that cube into the box the traversal uses.
  */
 #include "vxo.h"
 #include <stdlib.h>
@@ -155,4 +155,69 @@ void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct
 #undef I3
     free(g1);
     free(g2);
+}
+
+/* ---- vxo_field_box: the cube r grown to per-axis extents ----
+ * Solid = non-air (colour byte != 0); cells outside the grid count as air.
+ * ex = max e in [r, cap-1] with box (e, r, r) empty, then ey with (ex, e, r),
+ * then ez with (ex, ey, e).  Emptiness is monotone in each extent, so the
+ * maximum is found by bisection (the kernel's k_oct_box does the same). */
+typedef struct { int X, Y, Z; const int *S; } bctx;
+
+static inline size_t PS(const bctx *b, int x, int y, int z) {
+    return (size_t)x + (size_t)(b->X + 1) * ((size_t)y + (size_t)(b->Y + 1) * (size_t)z);
+}
+/* solid cells in the inclusive box between corners a and a + e*s */
+static int box_solid(const bctx *b, int x, int y, int z, const int s[3], const int e[3]) {
+    int lo[3] = {x, y, z}, hi[3] = {x + s[0] * e[0], y + s[1] * e[1], z + s[2] * e[2]};
+    const int dim[3] = {b->X, b->Y, b->Z};
+    for (int i = 0; i < 3; i++) {
+        if (lo[i] > hi[i]) { const int t = lo[i]; lo[i] = hi[i]; hi[i] = t; }
+        if (lo[i] < 0) lo[i] = 0;
+        if (hi[i] > dim[i] - 1) hi[i] = dim[i] - 1;
+        if (lo[i] > hi[i]) return 0;
+        hi[i]++;
+    }
+    return b->S[PS(b, hi[0], hi[1], hi[2])] - b->S[PS(b, lo[0], hi[1], hi[2])] - b->S[PS(b, hi[0], lo[1], hi[2])] -
+           b->S[PS(b, hi[0], hi[1], lo[2])] + b->S[PS(b, lo[0], lo[1], hi[2])] + b->S[PS(b, lo[0], hi[1], lo[2])] +
+           b->S[PS(b, hi[0], lo[1], lo[2])] - b->S[PS(b, lo[0], lo[1], lo[2])];
+}
+
+void vxo_field_box(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, const uint8_t *r_cube,
+                   uint8_t *e_out) {
+    int *S = (int *)calloc((size_t)(X + 1) * (Y + 1) * (Z + 1), sizeof(int));
+    bctx b = {X, Y, Z, S};
+    for (int z = 1; z <= Z; z++)
+        for (int y = 1; y <= Y; y++)
+            for (int x = 1; x <= X; x++) {
+                const size_t c = (size_t)(x - 1) + (size_t)X * ((size_t)(y - 1) + (size_t)Y * (size_t)(z - 1));
+                S[PS(&b, x, y, z)] = (rgba[4 * c + 2] != 0) + S[PS(&b, x - 1, y, z)] + S[PS(&b, x, y - 1, z)] +
+                                     S[PS(&b, x, y, z - 1)] - S[PS(&b, x - 1, y - 1, z)] - S[PS(&b, x - 1, y, z - 1)] -
+                                     S[PS(&b, x, y - 1, z - 1)] + S[PS(&b, x - 1, y - 1, z - 1)];
+            }
+    const int s[3] = {oct & 1 ? -1 : 1, oct & 2 ? -1 : 1, oct & 4 ? -1 : 1};
+#pragma omp parallel for schedule(static)
+    for (int z = 0; z < Z; z++)
+        for (int y = 0; y < Y; y++)
+            for (int x = 0; x < X; x++) {
+                const size_t c = (size_t)x + (size_t)X * ((size_t)y + (size_t)Y * (size_t)z);
+                int e[3] = {0, 0, 0};
+                if (rgba[4 * c + 2] == 0) {
+                    const int r = r_cube[c];
+                    e[0] = e[1] = e[2] = r;
+                    for (int a = 0; a < 3; a++) {
+                        int lo = r, hi = cap - 1;          /* lo: known empty */
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) / 2;
+                            e[a] = mid;
+                            if (box_solid(&b, x, y, z, s, e) == 0) lo = mid; else hi = mid - 1;
+                        }
+                        e[a] = lo;
+                    }
+                }
+                e_out[3 * c] = (uint8_t)e[0];
+                e_out[3 * c + 1] = (uint8_t)e[1];
+                e_out[3 * c + 2] = (uint8_t)e[2];
+            }
+    free(S);
 }

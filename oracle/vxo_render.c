@@ -270,9 +270,10 @@ static inline int in_grid(const vxo_scene *s, const int a[3]) {
     return a[0] >= 0 && a[1] >= 0 && a[2] >= 0 && a[0] < s->X && a[1] < s->Y && a[2] < s->Z;
 }
 
-/* Octant-cube walk of the ray B + o + t*d (B an integer cell, camera- or
+/* Octant-box walk of the ray B + o + t*d (B an integer cell, camera- or
  * origin-relative cells c) from the start cell B + c to the first colour
- * change.  glass_layer != 0: a glass entry is recorded and the walk goes on to
+ * change: from cell c the box [c, c + e*s] (vxo_field_box extents of the ray
+ * octant) is all air, so the ray jumps to where it leaves the box.  glass_layer != 0: a glass entry is recorded and the walk goes on to
  * the next change behind it (primary visibility); 0: the first change ends
  * the walk (reflection rays).  A start cell outside the grid is sky. */
 static int walk(const vxo_scene *s, const int cc[3], const float o[3], const float d[3], int c[3],
@@ -289,24 +290,29 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
     const uint8_t *tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
     (*fetches)++;
     const int oct = (d[0] < 0.0f ? 1 : 0) | (d[1] < 0.0f ? 2 : 0) | (d[2] < 0.0f ? 4 : 0);
-    const uint8_t *octr = s->oct_r[oct];
-#define OCT_R(a) ((int)octr[(size_t)(a)[0] + (size_t)s->X * ((size_t)(a)[1] + (size_t)s->Y * (size_t)(a)[2])])
+    const uint8_t *octe = s->oct_e[oct];
+#define OCT_E(a, e)                                                                                  \
+    do {                                                                                             \
+        const uint8_t *p_ = octe + 3 * ((size_t)(a)[0] + (size_t)s->X * ((size_t)(a)[1] + (size_t)s->Y * (size_t)(a)[2])); \
+        (e)[0] = p_[0]; (e)[1] = p_[1]; (e)[2] = p_[2];                                              \
+    } while (0)
     int prev = tx[2];
-    int R = OCT_R(abs_c);
+    int E[3];
+    OCT_E(abs_c, E);
     int nrec = 0;
     const int cap = 4 * (dims[0] + dims[1] + dims[2]);
     for (int iter = 0; iter < cap; iter++) {
         float tb[3];
         for (int i = 0; i < 3; i++)
-            tb[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? R + 1 : -R)) - o[i]) * inv[i] : INFINITY;
+            tb[i] = d[i] != 0.0f ? ((float)(c[i] + (stp[i] > 0 ? E[i] + 1 : -E[i])) - o[i]) * inv[i] : INFINITY;
         const int a = (tb[0] <= tb[1] && tb[0] <= tb[2]) ? 0 : (tb[1] <= tb[2] ? 1 : 2);
         const float te = tb[a];
         for (int i = 0; i < 3; i++) {
             if (i == a) {
-                c[i] = c[i] + stp[i] * (R + 1);
+                c[i] = c[i] + stp[i] * (E[i] + 1);
             } else {
                 const int v = g_f2i(floorf(o[i] + te * d[i]));
-                const int lo = d[i] < 0.0f ? c[i] - R : c[i], hi = d[i] < 0.0f ? c[i] : c[i] + R;
+                const int lo = d[i] < 0.0f ? c[i] - E[i] : c[i], hi = d[i] < 0.0f ? c[i] : c[i] + E[i];
                 c[i] = v < lo ? lo : (v > hi ? hi : v);
             }
         }
@@ -315,7 +321,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
         tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
         (*fetches)++;
         const int col = tx[2];
-        R = OCT_R(abs_c);                          /* air cube ahead */
+        OCT_E(abs_c, E);                           /* air box ahead */
         if (col != prev) {
             vxo_gbuf *h = &g[nrec];
             h->color = col;
@@ -338,7 +344,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
     }
     *cap_hit = 1;
     return nrec;
-#undef OCT_R
+#undef OCT_E
 }
 
 int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],

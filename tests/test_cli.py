@@ -9,6 +9,8 @@ import subprocess
 import numpy as np
 import pytest
 
+from voxmap_amd import _abi
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(ROOT, "voxmap_amd", "vxrender")
 KEY = "q83vEjRWeJCrze8SNFZ4kKvN7xI0VniQq83vEjRWeJA"   # test key (not the reference's)
@@ -16,7 +18,7 @@ KEY = "q83vEjRWeJCrze8SNFZ4kKvN7xI0VniQq83vEjRWeJA"   # test key (not the refere
 
 def test_cli_help_and_errors(built):
     r = subprocess.run([CLI, "--help"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0 and "ABI version 2" in r.stdout
+    assert r.returncode == 0 and f"ABI version {_abi.ABI_VERSION}" in r.stdout
     r = subprocess.run([CLI, "--map", "/nonexistent/map.bin"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "cannot open" in r.stderr
     r = subprocess.run([CLI, "--bogus"], capture_output=True, text=True, timeout=60)

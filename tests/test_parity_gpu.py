@@ -85,8 +85,11 @@ def test_field_octant_copies_match_oracle(noise, octant):
     field = vx.field_build(scenes.small_proc(17, dims=dims, n_boxes=24, n_glass=4))
     with _scene(vx, field, noise, dims) as sc:
         dev = sc.read_field(octant)
+        box = sc.read_boxes(octant)
     assert np.array_equal(dev[..., :3], field[..., :3])
     assert np.array_equal(dev[..., 3], oracle.field_octant(field, octant, 32))
+    assert np.array_equal(box[..., 0], field[..., 2])
+    assert np.array_equal(box[..., 1:], oracle.field_box(field, octant, 32))
 
 
 @pytest.fixture(scope="module")
@@ -320,10 +323,10 @@ def test_c5_rows_soft_shadows_full_quality(noise):
                   noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
         img, st = sc.render(fr, stats=True)
         field = sc.read_field(0)
-        oct_r = [np.ascontiguousarray(field[..., 3])] + [np.ascontiguousarray(sc.read_field(o)[..., 3])
-                                                        for o in range(1, 8)]
+        # the device's octant boxes (checked against oracle.field_box on smaller fields)
+        oct_e = [np.ascontiguousarray(sc.read_boxes(o)[..., 1:]) for o in range(8)]
     step = 271
-    ref, _ = oracle.Oracle(field, noise, oct_r=oct_r).render(fr.params, c["w"], c["h"], row0=step // 2,
+    ref, _ = oracle.Oracle(field, noise, oct_e=oct_e).render(fr.params, c["w"], c["h"], row0=step // 2,
                                                             row_step=step, threads=16)
     rows = np.arange(step // 2, c["h"], step)
     _compare(img, ref, rows)

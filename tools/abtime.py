@@ -44,7 +44,10 @@ def main():
         label, path = spec.split("=", 1)
         L = C.CDLL(os.path.abspath(path))
         for name, res, argt in _abi.SIGNATURES:
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:      # an older ABI: only the symbols used here are needed
+                continue
             fn.restype, fn.argtypes = res, argt
         d = _abi.SceneDesc()
         buf = C.create_string_buffer(gbytes, len(gbytes))

@@ -28,7 +28,7 @@ FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
 FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
 FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary index path
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class SceneDesc(C.Structure):
@@ -78,6 +78,7 @@ SIGNATURES = [
     ("vx_scene_destroy", None, [C.c_void_p]),
     ("vx_scene_read_field", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("vx_scene_read_field_copy", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    ("vx_scene_read_boxes", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("vx_scene_dims", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     ("vx_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
                             C.c_void_p, C.c_int, C.c_void_p, C.POINTER(Stats)]),

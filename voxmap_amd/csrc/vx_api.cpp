@@ -40,7 +40,7 @@ struct vx_scene {
     int device = 0;
     int X = 0, Y = 0, Z = 0;
     int noise_w = 0, noise_h = 0;
-    uint16_t *d_prim = nullptr;   // 8 padded octant copies (vx_internal.h FieldLayout)
+    uint32_t *d_prim = nullptr;   // 8 padded octant copies (vx_internal.h FieldLayout)
     uint8_t *d_sun = nullptr;     // R, G channels
     int8_t *d_sunp = nullptr;     // R, G channels, int8, -1 border (Z <= 126)
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
@@ -186,10 +186,13 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     // and from there into that octant's prim copy (border = sentinel)
     const size_t N = (size_t)X * Y * Z;
     int lrc = 0;
-    if ((e = hipMalloc(&s->d_prim, 8 * L.texels * 2)) == hipSuccess &&
+    int *psum = nullptr;   // prefix sums of solid cells for the octant boxes
+    if ((e = hipMalloc(&s->d_prim, 8 * L.texels * 4)) == hipSuccess &&
         (e = hipMalloc(&s->d_sun, 2 * N)) == hipSuccess && (e = hipMalloc(&s->d_rg, 2 * N)) == hipSuccess &&
-        (e = hipMemsetD16Async((hipDeviceptr_t)s->d_prim, 0xFFFFu, 8 * L.texels, s->stream)) == hipSuccess) {
-        lrc = launch_field_pack(lin, nullptr, s->d_sun, s->d_rg, X, Y, Z, L.pad, s->stream);
+        (e = hipMalloc(&psum, sizeof(int) * (size_t)(X + 1) * (Y + 1) * (Z + 1))) == hipSuccess &&
+        (e = hipMemsetD32Async((hipDeviceptr_t)s->d_prim, 0xFFFFFFFF, 8 * L.texels, s->stream)) == hipSuccess) {
+        lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
+        if (!lrc) lrc = launch_field_psum(lin, psum, X, Y, Z, s->stream);
         // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
         // march's loaded value carries the exit test (vx_kernels.hip march_fast); values <= Z <= 126
         if (!lrc && Z <= 126 && (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2)) < (1u << 24)) {
@@ -203,10 +206,11 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         }
         for (int oct = 0; oct < 8 && !lrc; oct++) {
             lrc = launch_field_octant(lin, X, Y, Z, cap, oct, ga, gb, s->stream);
-            if (!lrc) lrc = launch_field_pack(lin, s->d_prim + oct * L.texels, nullptr, nullptr, X, Y, Z, L.pad, s->stream);
+            if (!lrc) lrc = launch_field_box(lin, psum, s->d_prim + oct * L.texels, X, Y, Z, L.pad, cap, oct, s->stream);
         }
         e = hipStreamSynchronize(s->stream);
     }
+    if (psum) (void)hipFree(psum);
     (void)hipFree(ga);
     (void)hipFree(gb);
     (void)hipFree(lin);
@@ -244,21 +248,29 @@ int vx_scene_dims(const vx_scene *s, int dims[3]) {
 
 int vx_scene_read_field(vx_scene *s, void *host_out, size_t cap) { return vx_scene_read_field_copy(s, 0, host_out, cap); }
 
-int vx_scene_read_field_copy(vx_scene *s, int octant, void *host_out, size_t cap) {
-    if (!s || !host_out) return set_error(VX_EINVAL, "vx_scene_read_field: null argument");
-    if (octant < 0 || octant > 7) return set_error(VX_EINVAL, "vx_scene_read_field_copy: octant must be 0..7");
+static int read_copy(vx_scene *s, int octant, void *host_out, size_t cap, bool boxes, const char *what) {
+    if (!s || !host_out) return set_error(VX_EINVAL, std::string(what) + ": null argument");
+    if (octant < 0 || octant > 7) return set_error(VX_EINVAL, std::string(what) + ": octant must be 0..7");
     const size_t n = (size_t)s->X * s->Y * s->Z * 4;
-    if (cap < n) return set_error(VX_EINVAL, "vx_scene_read_field: buffer too small");
+    if (cap < n) return set_error(VX_EINVAL, std::string(what) + ": buffer too small");
     VX_HIP(hipSetDevice(s->device));
     uint32_t *lin = nullptr;
     VX_HIP(hipMalloc(&lin, n));
-    hipError_t e = (hipError_t)launch_field_unpack(s->d_rg, s->d_prim + (size_t)octant * s->L.texels, lin, s->X, s->Y,
-                                                   s->Z, s->L.pad, s->stream);
+    hipError_t e = (hipError_t)launch_field_unpack(boxes ? nullptr : s->d_rg, s->d_prim + (size_t)octant * s->L.texels,
+                                                   lin, s->X, s->Y, s->Z, s->L.pad, s->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, lin, n, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(lin);
-    if (e != hipSuccess) return set_error(VX_EDEVICE, std::string("vx_scene_read_field: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return set_error(VX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
     return VX_OK;
+}
+
+int vx_scene_read_field_copy(vx_scene *s, int octant, void *host_out, size_t cap) {
+    return read_copy(s, octant, host_out, cap, false, "vx_scene_read_field");
+}
+
+int vx_scene_read_boxes(vx_scene *s, int octant, void *host_out, size_t cap) {
+    return read_copy(s, octant, host_out, cap, true, "vx_scene_read_boxes");
 }
 
 static int check_params(const vx_scene *s, const vx_frame_params *p, int w, int h, int fmt) {
@@ -348,17 +360,17 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.kcam = (unsigned)(p->cam_cell[0] + s->L.pad) + (unsigned)a.Xp * (unsigned)(p->cam_cell[1] + s->L.pad) +
              a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);   // mod 2^32
     {
-        // fp32 x/y index: 2*(x + Xp*y) of a fetched cell lies in [0, 2*Xp*Yp),
-        // its partial sums 2x in [0, 2Xp) and y in [0, Yp), all exact fp32
-        // integers below 2^24; the 24-bit multiply needs 2*Xp*Yp < 2^23, the
+        // fp32 x/y index: 4*(x + Xp*y) of a fetched cell lies in [0, 4*Xp*Yp),
+        // its partial sums 4x in [0, 4Xp) and y in [0, Yp), all exact fp32
+        // integers below 2^24; the 24-bit multiply needs 4*Xp*Yp < 2^23, the
         // 32-bit byte offsets all 8 copies below 4 GiB
-        const double xy2 = 2.0 * (double)s->L.Xp * (double)s->L.Yp;
-        const bool ok = xy2 < 8388608.0 && 16.0 * (double)s->L.texels < 4294967296.0 &&
+        const double xy4 = 4.0 * (double)s->L.Xp * (double)s->L.Yp;
+        const bool ok = xy4 < 8388608.0 && 32.0 * (double)s->L.texels < 4294967296.0 &&
                         std::abs(p->cam_cell[0]) < (1 << 21) && std::abs(p->cam_cell[1]) < (1 << 21);
         a.prim_f32 = ok && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
-        a.kx2 = (float)(2 * (p->cam_cell[0] + s->L.pad));
+        a.kx4 = (float)(4 * (p->cam_cell[0] + s->L.pad));
         a.ky = (float)(p->cam_cell[1] + s->L.pad);
-        a.kz = 2u * a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);
+        a.kz = 4u * a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);
     }
 
     if (stats) {

@@ -50,7 +50,7 @@ struct FrameConsts {
 
 // Parameters of one render launch (passed by value to the kernel).
 struct KernelArgs {
-    const uint16_t *prim;    // 8 padded octant copies: colour | cube size << 8 (FieldLayout)
+    const uint32_t *prim;    // 8 padded octant copies: colour | ex << 8 | ey << 16 | ez << 24 (FieldLayout)
     const uint8_t *sun;      // R channel then G channel, X*Y*Z bytes each
     const int8_t *sunp;      // R then G, int8, inside a border of SB cells of -1 (nullptr: Z > 126)
     int SB;                  // border width of sunp (Z + 2: a march step moves <= Z + 1 cells per axis)
@@ -79,11 +79,11 @@ struct KernelArgs {
     unsigned kcam;           // padded index of the camera cell, mod 2^32
     FrameConsts fc;
     // fp32 x/y primary index (vx_render decides): byte offset
-    // from prim = cvt(fma(2Xp, h1 + ky, fma(2, h0, kx2))) + 2XpYp*(int)h2 + kz2
-    // (mod 2^32), exact while 2*Xp*Yp < 2^23 and the 8 copies < 4 GiB
+    // from prim = cvt(fma(4Xp, h1 + ky, fma(4, h0, kx4))) + 4XpYp*(int)h2 + kz
+    // (mod 2^32), exact while 4*Xp*Yp < 2^23 and the 8 copies < 4 GiB
     int prim_f32;            // 0: the integer index path
-    float kx2, ky;           // 2*(camera padded x), camera padded y (ray octant terms added per lane)
-    unsigned kz;             // 2*XpYp*(camera padded z), mod 2^32
+    float kx4, ky;           // 4*(camera padded x), camera padded y (ray octant terms added per lane)
+    unsigned kz;             // 4*XpYp*(camera padded z), mod 2^32
 };
 
 void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, int max_steps, FrameConsts &fc);
@@ -94,9 +94,9 @@ enum StatSlot {
 };
 
 // Field data in HBM (vx_kernels.hip): `prim` = 8 copies (one
-// per ray octant) of the X x Y x Z grid, u16 colour | air-cube size << 8,
-// inside a border of pad = cap sentinel cells; `sun` = R and G channels (u8);
-// `rg` = R | G << 8 (u16).
+// per ray octant) of the X x Y x Z grid, u32 colour | air-box extents << 8,
+// 16, 24, inside a border of pad = cap sentinel cells; `sun` = R and G
+// channels (u8); `rg` = R | G << 8 (u16).
 struct FieldLayout {
     int pad, Xp, Yp, Zp;
     size_t texels;           // Xp * Yp * Zp, one prim copy
@@ -104,11 +104,15 @@ struct FieldLayout {
 FieldLayout field_layout(int X, int Y, int Z, int cap);
 // padded int8 sun channels (border = -1) from the linear RGBA upload
 int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int SB, void *stream);
-// linear RGBA upload (A = an octant's cube sizes) -> prim copy; -> sun, rg (either may be null)
-int launch_field_pack(const uint32_t *lin, uint16_t *prim_copy, uint8_t *sun, uint16_t *rg, int X, int Y, int Z,
-                      int pad, void *stream);
+// linear RGBA upload -> sun, rg
+int launch_field_pack(const uint32_t *lin, uint8_t *sun, uint16_t *rg, int X, int Y, int Z, void *stream);
+// prefix sums of solid cells of the upload, (X+1)(Y+1)(Z+1) ints
+int launch_field_psum(const uint32_t *lin, int *S, int X, int Y, int Z, void *stream);
+// upload with A = an octant's cube sizes (launch_field_octant) -> that octant's prim copy (boxes)
+int launch_field_box(const uint32_t *lin, const int *S, uint32_t *prim_copy, int X, int Y, int Z, int pad, int cap,
+                     int oct, void *stream);
 // RGBA of one octant copy, linear
-int launch_field_unpack(const uint16_t *rg, const uint16_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
+int launch_field_unpack(const uint16_t *rg, const uint32_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
                         void *stream);
 
 // Launchers (vx_kernels.hip).  Return a hipError_t as int.

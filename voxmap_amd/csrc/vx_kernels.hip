@@ -137,11 +137,21 @@ struct Counters {
     unsigned prim_witers, march_witers;      // loop iterations per wave (diagnostic: lane utilisation)
 };
 
-// (float)((t >> 8) & 0xff) as one v_cvt_f32_ubyte1 (the compiler folds the
-// mask away when it knows t < 2^16 and then emits a shift + convert)
+// (float)((t >> 8k) & 0xff) as one v_cvt_f32_ubyteK (left to itself the
+// compiler may fold the mask away and emit a shift + convert)
 __device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+__device__ __forceinline__ float cvt_f32_ubyte2(uint32_t t) {
+    float r;
+    asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+__device__ __forceinline__ float cvt_f32_ubyte3(uint32_t t) {
+    float r;
+    asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
 
@@ -153,16 +163,17 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 
 // Field data in HBM, each array shaped for the loop that
 // reads it, so a cache line holds as many useful cells as possible:
-//   prim  8 copies, one per ray octant, u16 per cell: colour | air-cube size
-//         << 8, inside a border of P = cap sentinel cells (0xFFFF: size 255,
-//         never real, sizes are <= cap - 1 <= 254), so the primary traversal
-//         detects leaving the grid from the value it loads;
+//   prim  8 copies, one per ray octant, u32 per cell: colour | ex << 8 |
+//         ey << 16 | ez << 24, the extents of the all-air box ahead (vxo_field_box),
+//         inside a border of P = cap sentinel cells (0xFFFFFFFF: colour 0xFF is
+//         no palette index, extents are <= cap - 1 <= 254), so the primary
+//         traversal detects leaving the grid from the value it loads;
 //   sun   map.bin's R ("up") and G ("down") channels, u8 each, linear: the
 //         sun march reads one of them;
 //   rg    R | G << 8, u16, linear: the AO trilinear sample.
 // Every read is in bounds: the traversal stays within P of the grid, march()
 // returns before reading outside it, the AO sample clamps.
-constexpr uint32_t kSentinel = 0xFF00u;   // border cells hold 0xFFFF: size 255, colour 0xFF
+constexpr uint32_t kSentinel = 0xFFFFFFFFu;   // border cells: colour 0xFF, extents 255
 
 // Loads at a 32-bit byte offset from a wave-uniform base: lets the compiler
 // use the saddr form (SGPR base + VGPR offset) instead of 64-bit per-lane
@@ -368,20 +379,19 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, i
 // First in-grid colour change along the view ray = the nearest front face of
 // the greedy mesh of sdf.cpp:281-356 after back-face culling.  Box-exit
 // stepping (oracle/vxo_render.c vxo_primary): in the ray octant's field copy
-// the A byte R of a cell says the cube [c, c + R*s] ahead of it is air, so
-// one step goes to the face where the ray leaves that cube (R = 0: an exact
-// DDA step).  Returns 0 sky, 1 surface, 2 glass + what is behind.
+// the extents E of a cell say the box [c, c + E*s] ahead of it is air, so one
+// step goes to the face where the ray leaves that box (E = 0: an exact DDA
+// step).  Returns 0 sky, 1 surface, 2 glass + what is behind.
 //
 // The loop runs on camera-relative cells held as fp32 integers (exact: the
 // host keeps |cam_cell| < 2^22), with x and y in packed-fp32 pairs:
 //   h = c + hp (hp = 1 on a positive axis, 0 on a negative one), s = +-1;
-//   far face    A  = c + (s > 0 ? R + 1 : -R) = fma(s, R, h)       (exact)
+//   far face    A  = c + (s > 0 ? E + 1 : -E) = fma(s, E, h)       (exact, per axis)
 //   crossing    tb = (A - o) * iv                                   (= oracle)
-//   exit axis   next h = A + s; others med3(floor(o + te*d) + hp, h - R, h + R)
+//   exit axis   next h = A + s; others med3(floor(o + te*d) + hp, h, A)
 // d == 0 is a positive axis with iv = +inf: A - o >= 1 - o > 0 (0 <= o < 1 is
-// checked by vx_render), so tb = +inf exactly as the oracle's.  The cube
-// [c, c + R*s] lies ahead of the ray: clamp range [h, h + R] on a positive
-// axis, [h - R, h] on a negative one, i.e. [fma(hp - 1, R, h), fma(hp, R, h)].
+// checked by vx_render), so tb = +inf exactly as the oracle's.  The box
+// [c, c + E*s] lies ahead of the ray: h and A bracket it on every axis.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <bool F32IDX>
@@ -418,28 +428,28 @@ __device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d
     float h0 = (float)(c0 + ip0), h1 = (float)(c1 + ip1), h2 = (float)(c2 + ip2);
     // padded index of h: kray + hx + Xp*hy + XpYp*hz, mod 2^32 with 24-bit
     // signed products (|h| < 2^23)
-    const uint16_t *ppad = a.prim + (size_t)oct * a.copy_texels;
+    const uint32_t *ppad = a.prim + (size_t)oct * a.copy_texels;
     const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
-    // F32IDX (a.prim_f32): 2*(x + Xp*y) in fp32 (exact, < 2^23), z by a
-    // 24-bit multiply-add, a 32-bit byte offset from a.prim: 2 fma + add +
-    // 2 cvt + mad24 + add instead of 3 cvt + 2 mul24 + add3 + a 64-bit add
-    const float kx2 = a.kx2 - (float)(2 * ip0), ky = a.ky - (float)ip1;
-    const float fXp2 = (float)(2 * a.Xp);
-    const int XpYp2 = (int)(2u * a.XpYp);
-    const unsigned kz = a.kz - (unsigned)XpYp2 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 1);
+    // F32IDX (a.prim_f32): the byte offset 4*(x + Xp*y) in fp32 (exact, <
+    // 2^23), z by a 24-bit multiply-add, 32 bits from a.prim: 2 fma + add + 2
+    // cvt + mad24 + add instead of 3 cvt + 2 mul24 + add3 + a 64-bit add
+    const float kx4 = a.kx4 - (float)(4 * ip0), ky = a.ky - (float)ip1;
+    const float fXp4 = (float)(4 * a.Xp);
+    const int XpYp4 = (int)(4u * a.XpYp);
+    const unsigned kz = a.kz - (unsigned)XpYp4 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 2);
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         if (F32IDX) {
-            const float xy = __builtin_fmaf(fXp2, y + ky, __builtin_fmaf(2.0f, x, kx2));
-            const unsigned off = (unsigned)(int)xy + ((unsigned)__mul24(XpYp2, (int)z) + kz);
-            return (uint32_t)ld_off(a.prim, off);
+            const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
+            const unsigned off = (unsigned)(int)xy + ((unsigned)__mul24(XpYp4, (int)z) + kz);
+            return ld_off(a.prim, off);
         }
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
-        return (uint32_t)ppad[(unsigned)idx];
+        return ppad[(unsigned)idx];
     };
     uint32_t t = fetch(h0, h1, h2);
     cnt.prim_fetch++;
     int prev = t & 0xff;
-    float R = cvt_f32_ubyte1(t);
+    float E0 = cvt_f32_ubyte1(t), E1 = cvt_f32_ubyte2(t), E2 = cvt_f32_ubyte3(t);
     // gmark: the colour whose entry is "the first glass" -- glass until a glass
     // entry is recorded, then 256 (matches nothing).  The sentinel's colour
     // byte 0xFF is no palette index (vx_scene_create), so leaving the grid is
@@ -453,15 +463,15 @@ __device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d
     float pad_acc = 0.0f;
     do {
         VX_PAD(VX_PAD_PRIM, pad_acc)
-        // far face of the air cube [c, c + R*s] ahead: A = h + s*R (exact)
-        const float A0 = __builtin_fmaf(s0, R, h0), A1 = __builtin_fmaf(s1, R, h1), A2 = __builtin_fmaf(s2, R, h2);
+        // far face of the air box [c, c + E*s] ahead: A = h + s*E (exact)
+        const float A0 = __builtin_fmaf(s0, E0, h0), A1 = __builtin_fmaf(s1, E1, h1), A2 = __builtin_fmaf(s2, E2, h2);
         tb0 = (A0 - o0) * iv0;
         tb1 = (A1 - o1) * iv1;
         tb2 = (A2 - o2) * iv2;
         te = __builtin_fminf(__builtin_fminf(tb0, tb1), tb2);
         const bool e0 = tb0 == te;
         const bool e1 = !e0 && tb1 == te;
-        // other axes: floor(o + te*d) as h, clamped into the cube, whose h
+        // other axes: floor(o + te*d) as h, clamped into the box, whose h
         // range is [h, A] (positive axis) or [A, h] (negative): med3(q, h, A)
         const float q0 = floorf(o0 + te * d0) + hp0;
         const float q1 = floorf(o1 + te * d1) + hp1;
@@ -484,7 +494,7 @@ __device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
 #endif
         prev = col;
-        R = cvt_f32_ubyte1(t);
+        E0 = cvt_f32_ubyte1(t); E1 = cvt_f32_ubyte2(t); E2 = cvt_f32_ubyte3(t);
         cnt.prim_witers += once_per_wave(1u);      // counted in the loop: it stays a scalar
     } while (stop == 0 && ++it < cap);
     if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
@@ -807,7 +817,7 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
 __device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o0, float o1, float o2, float d0,
                             float d1, float d2, int c0, int c1, int c2, Surf &h, Counters &cnt) {
     const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
-    const uint16_t *pp = a.prim + (size_t)oct * a.copy_texels;
+    const uint32_t *pp = a.prim + (size_t)oct * a.copy_texels;
     auto inside = [&](int x, int y, int z) {
         return (unsigned)x < (unsigned)a.X && (unsigned)y < (unsigned)a.Y && (unsigned)z < (unsigned)a.Z;
     };
@@ -821,29 +831,29 @@ __device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o
     if (!inside(x, y, z)) return 0;
     uint32_t t = fetch(x, y, z);
     cnt.refl_fetch++;
-    int prev = t & 0xff, R = (int)(t >> 8);
+    int prev = t & 0xff, e0 = (int)((t >> 8) & 0xff), e1 = (int)((t >> 16) & 0xff), e2 = (int)(t >> 24);
     const int cap = 4 * (a.X + a.Y + a.Z);
     for (int it = 0; it < cap; it++) {
-        const float tb0 = d0 != 0.0f ? ((float)(c0 + (st0 > 0 ? R + 1 : -R)) - o0) * iv0 : kInf;
-        const float tb1 = d1 != 0.0f ? ((float)(c1 + (st1 > 0 ? R + 1 : -R)) - o1) * iv1 : kInf;
-        const float tb2 = d2 != 0.0f ? ((float)(c2 + (st2 > 0 ? R + 1 : -R)) - o2) * iv2 : kInf;
+        const float tb0 = d0 != 0.0f ? ((float)(c0 + (st0 > 0 ? e0 + 1 : -e0)) - o0) * iv0 : kInf;
+        const float tb1 = d1 != 0.0f ? ((float)(c1 + (st1 > 0 ? e1 + 1 : -e1)) - o1) * iv1 : kInf;
+        const float tb2 = d2 != 0.0f ? ((float)(c2 + (st2 > 0 ? e2 + 1 : -e2)) - o2) * iv2 : kInf;
         const int ax = (tb0 <= tb1 && tb0 <= tb2) ? 0 : (tb1 <= tb2 ? 1 : 2);
         const float te = ax == 0 ? tb0 : (ax == 1 ? tb1 : tb2);
-        auto side = [&](int c, float o, float d) {
+        auto side = [&](int c, float o, float d, int e) {
             const int v = f2i(floorf(o + te * d));
-            const int lo = d < 0.0f ? c - R : c, hi = d < 0.0f ? c : c + R;
+            const int lo = d < 0.0f ? c - e : c, hi = d < 0.0f ? c : c + e;
             return v < lo ? lo : (v > hi ? hi : v);
         };
-        const int n0 = ax == 0 ? c0 + st0 * (R + 1) : side(c0, o0, d0);
-        const int n1 = ax == 1 ? c1 + st1 * (R + 1) : side(c1, o1, d1);
-        const int n2 = ax == 2 ? c2 + st2 * (R + 1) : side(c2, o2, d2);
+        const int n0 = ax == 0 ? c0 + st0 * (e0 + 1) : side(c0, o0, d0, e0);
+        const int n1 = ax == 1 ? c1 + st1 * (e1 + 1) : side(c1, o1, d1, e1);
+        const int n2 = ax == 2 ? c2 + st2 * (e2 + 1) : side(c2, o2, d2, e2);
         c0 = n0; c1 = n1; c2 = n2;
         x = B0 + c0; y = B1 + c1; z = B2 + c2;
         if (!inside(x, y, z)) return 0;
         t = fetch(x, y, z);
         cnt.refl_fetch++;
         const int col = t & 0xff;
-        R = (int)(t >> 8);
+        e0 = (int)((t >> 8) & 0xff); e1 = (int)((t >> 16) & 0xff); e2 = (int)(t >> 24);
         if (col != prev) {
             const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
             h.color = col;
@@ -1173,14 +1183,82 @@ int launch_detile(const void *tiles, void *frame, int w, int h, int ts, int tile
 }
 
 namespace {
-// linear RGBA upload (A = one octant's cube sizes) -> that octant's prim copy
-__global__ void k_pack_prim(const uint32_t *src, uint16_t *dst, int X, int Y, int Z, int P) {
+// ---- prefix sums of solid (non-air) cells, S[(X+1)(Y+1)(Z+1)], S(0, ., .) =
+// S(., 0, .) = S(., ., 0) = 0: any box's solid count in 8 loads (k_oct_box)
+__device__ __forceinline__ size_t ps_index(int x, int y, int z, int X, int Y) {
+    return (size_t)x + (size_t)(X + 1) * ((size_t)y + (size_t)(Y + 1) * (size_t)z);
+}
+__global__ void k_psum_x(const uint32_t *lin, int *S, int X, int Y, int Z) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;     // (y, z) row of S
+    if (i >= (size_t)(Y + 1) * (Z + 1)) return;
+    const int y = (int)(i % (Y + 1)), z = (int)(i / (Y + 1));
+    int acc = 0;
+    S[ps_index(0, y, z, X, Y)] = 0;
+    for (int x = 1; x <= X; x++) {
+        if (y > 0 && z > 0)
+            acc += ((lin[(size_t)(x - 1) + (size_t)X * ((size_t)(y - 1) + (size_t)Y * (size_t)(z - 1))] >> 16) & 0xffu) != 0;
+        S[ps_index(x, y, z, X, Y)] = acc;
+    }
+}
+__global__ void k_psum_yz(int *S, int X, int Y, int Z, int axis) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;     // x fastest: coalesced
+    const int n = axis == 1 ? Y : Z, m = axis == 1 ? Z : Y;
+    if (i >= (size_t)(X + 1) * (m + 1)) return;
+    const int x = (int)(i % (X + 1)), j = (int)(i / (X + 1));
+    int acc = 0;
+    for (int k = 1; k <= n; k++) {
+        const size_t q = axis == 1 ? ps_index(x, k, j, X, Y) : ps_index(x, j, k, X, Y);
+        acc += S[q];
+        S[q] = acc;
+    }
+}
+
+// ---- one octant's prim copy: colour | ex << 8 | ey << 16 | ez << 24, the
+// cube r (A byte of the upload, k_oct_*) grown to the largest x extent, then
+// y, then z, each <= cap - 1, by bisection on box emptiness (oracle
+// vxo_field_box: the same definition, the same maxima)
+__global__ void k_oct_box(const uint32_t *lin, const int *S, uint32_t *dst, int X, int Y, int Z, int P, int cap,
+                          int sx, int sy, int sz) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+    const uint32_t t = lin[i];
+    const uint32_t col = (t >> 16) & 0xffu;
+    int e[3] = {0, 0, 0};
+    if (col == 0) {
+        const int r = (int)(t >> 24);
+        e[0] = e[1] = e[2] = r;
+        const int s[3] = {sx, sy, sz}, c[3] = {x, y, z}, dim[3] = {X, Y, Z};
+        auto solid = [&]() {
+            int lo[3], hi[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                int a0 = c[k], a1 = c[k] + s[k] * e[k];
+                if (a0 > a1) { const int tt = a0; a0 = a1; a1 = tt; }
+                a0 = a0 < 0 ? 0 : a0;
+                a1 = a1 > dim[k] - 1 ? dim[k] - 1 : a1;
+                if (a0 > a1) return 0;
+                lo[k] = a0;
+                hi[k] = a1 + 1;
+            }
+            return S[ps_index(hi[0], hi[1], hi[2], X, Y)] - S[ps_index(lo[0], hi[1], hi[2], X, Y)] -
+                   S[ps_index(hi[0], lo[1], hi[2], X, Y)] - S[ps_index(hi[0], hi[1], lo[2], X, Y)] +
+                   S[ps_index(lo[0], lo[1], hi[2], X, Y)] + S[ps_index(lo[0], hi[1], lo[2], X, Y)] +
+                   S[ps_index(hi[0], lo[1], lo[2], X, Y)] - S[ps_index(lo[0], lo[1], lo[2], X, Y)];
+        };
+        for (int k = 0; k < 3; k++) {
+            int lo = r, hi = cap - 1;                 // lo: known empty
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                e[k] = mid;
+                if (solid() == 0) lo = mid; else hi = mid - 1;
+            }
+            e[k] = lo;
+        }
+    }
     const size_t Xp = (size_t)X + 2 * P, Yp = (size_t)Y + 2 * P;
-    const uint32_t t = src[i];
-    dst[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))] = (uint16_t)(((t >> 16) & 0xffu) | ((t >> 24) << 8));
+    dst[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))] =
+        col | ((uint32_t)e[0] << 8) | ((uint32_t)e[1] << 16) | ((uint32_t)e[2] << 24);
 }
 // linear RGBA upload -> sun channel arrays and the AO array
 __global__ void k_pack_sun(const uint32_t *src, uint8_t *sun, uint16_t *rg, size_t N) {
@@ -1202,14 +1280,22 @@ __global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z
     sunp[j] = (int8_t)(t & 0xffu);
     sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);
 }
-// RGBA of one octant copy (R, G from rg; B, A from prim) for vx_scene_read_field_copy
-__global__ void k_unpack(const uint16_t *rg, const uint16_t *prim, uint32_t *dst, int X, int Y, int Z, int P) {
+// One octant copy, linear: RGBA (R, G from rg; B = colour; A = the cube size
+// = min(ex, ey, ez), since the box grows from the largest cube) for
+// vx_scene_read_field_copy, or the raw texels (rg == nullptr) for vx_scene_read_boxes
+__global__ void k_unpack(const uint16_t *rg, const uint32_t *prim, uint32_t *dst, int X, int Y, int Z, int P) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
     const size_t Xp = (size_t)X + 2 * P, Yp = (size_t)Y + 2 * P;
     const uint32_t p = prim[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))];
-    dst[i] = (uint32_t)rg[i] | ((p & 0xffu) << 16) | ((p >> 8) << 24);
+    if (!rg) {
+        dst[i] = p;
+        return;
+    }
+    const uint32_t e0 = (p >> 8) & 0xffu, e1 = (p >> 16) & 0xffu, e2 = p >> 24;
+    const uint32_t r = min(e0, min(e1, e2));
+    dst[i] = (uint32_t)rg[i] | ((p & 0xffu) << 16) | (r << 24);
 }
 }  // namespace
 
@@ -1223,12 +1309,28 @@ FieldLayout field_layout(int X, int Y, int Z, int cap) {
     return L;
 }
 
-int launch_field_pack(const uint32_t *lin, uint16_t *prim_copy, uint8_t *sun, uint16_t *rg, int X, int Y, int Z,
-                      int pad, void *stream) {
+int launch_field_pack(const uint32_t *lin, uint8_t *sun, uint16_t *rg, int X, int Y, int Z, void *stream) {
     const size_t N = (size_t)X * Y * Z;
     const dim3 grid((unsigned)((N + 255) / 256)), block(256);
-    if (prim_copy) hipLaunchKernelGGL(k_pack_prim, grid, block, 0, (hipStream_t)stream, lin, prim_copy, X, Y, Z, pad);
-    if (sun) hipLaunchKernelGGL(k_pack_sun, grid, block, 0, (hipStream_t)stream, lin, sun, rg, N);
+    hipLaunchKernelGGL(k_pack_sun, grid, block, 0, (hipStream_t)stream, lin, sun, rg, N);
+    return (int)hipGetLastError();
+}
+
+int launch_field_psum(const uint32_t *lin, int *S, int X, int Y, int Z, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const size_t nx = (size_t)(Y + 1) * (Z + 1), ny = (size_t)(X + 1) * (Z + 1), nz = (size_t)(X + 1) * (Y + 1);
+    hipLaunchKernelGGL(k_psum_x, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s, lin, S, X, Y, Z);
+    hipLaunchKernelGGL(k_psum_yz, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0, s, S, X, Y, Z, 1);
+    hipLaunchKernelGGL(k_psum_yz, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, s, S, X, Y, Z, 2);
+    return (int)hipGetLastError();
+}
+
+int launch_field_box(const uint32_t *lin, const int *S, uint32_t *prim_copy, int X, int Y, int Z, int pad, int cap,
+                     int oct, void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    const int sx = oct & 1 ? -1 : 1, sy = oct & 2 ? -1 : 1, sz = oct & 4 ? -1 : 1;
+    hipLaunchKernelGGL(k_oct_box, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lin, S,
+                       prim_copy, X, Y, Z, pad, cap, sx, sy, sz);
     return (int)hipGetLastError();
 }
 
@@ -1239,7 +1341,7 @@ int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int S
     return (int)hipGetLastError();
 }
 
-int launch_field_unpack(const uint16_t *rg, const uint16_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
+int launch_field_unpack(const uint16_t *rg, const uint32_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
                         void *stream) {
     const size_t N = (size_t)X * Y * Z;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, prim_copy,

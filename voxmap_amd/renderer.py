@@ -160,6 +160,13 @@ class Scene:
         check(lib().vx_scene_read_field_copy(self.handle, octant, out.ctypes.data, out.nbytes))
         return out
 
+    def read_boxes(self, octant: int = 0) -> np.ndarray:
+        """(Z, Y, X, 4) uint8: colour, ex, ey, ez of the octant's traversal boxes."""
+        X, Y, Z = self.dims
+        out = np.empty((Z, Y, X, 4), np.uint8)
+        check(lib().vx_scene_read_boxes(self.handle, octant, out.ctypes.data, out.nbytes))
+        return out
+
     def render(self, frame: Frame, *, pixel_format=_abi.PIXEL_RGBA32F, stats: bool = False):
         """Render to host memory; returns (image[h, w, 4], Stats or None)."""
         w, h = frame.width, frame.height
