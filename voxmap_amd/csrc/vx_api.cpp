@@ -377,10 +377,12 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
         a.stats = s->d_stats;
         VX_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(unsigned long long) * ST_COUNT * 64, st));
     }
-    VX_HIP(hipEventRecord(s->ev0, st));
+    // events only for the stats launch (kernel_ms): two extra stream packets
+    // per frame otherwise widen the gap between back-to-back frames
+    if (stats) VX_HIP(hipEventRecord(s->ev0, st));
     int rc = launch_render(a, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("render launch failed: ") + hipGetErrorString((hipError_t)rc));
-    VX_HIP(hipEventRecord(s->ev1, st));
+    if (stats) VX_HIP(hipEventRecord(s->ev1, st));
     if (stats) {
         unsigned long long v[ST_COUNT];
         VX_HIP(hipMemcpyAsync(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost, st));
