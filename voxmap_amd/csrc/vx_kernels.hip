@@ -619,6 +619,28 @@ __device__ __forceinline__ float div_shared(float a, float b, float y) {
 #ifndef VX_NORM_MK
 #define VX_NORM_MK 1
 #endif
+#ifndef VX_UNORM_MK
+#define VX_UNORM_MK 1
+#endif
+#ifndef VX_ROUGH_RCP
+#define VX_ROUGH_RCP 1
+#endif
+
+// RN(1/l) for l with |l| in [2^-40, 2^41): v_rcp + one Newton step equals the
+// IEEE reciprocal on every such input (tools/micro/rcp_check.hip, exhaustive
+// over exponents -40..40, both signs: profiles/r01_rcp_check.txt).  Callers
+// guarantee the range.
+__device__ __forceinline__ float rcp_ranged(float l) {
+    const float r = __builtin_amdgcn_rcpf(l);
+    return __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
+}
+
+// normalize3 of a vector whose length lies in [2^-40, 2^41) (exactly the IEEE result)
+__device__ __forceinline__ void normalize3_ranged(float v0, float v1, float v2, float &o0, float &o1, float &o2) {
+    const float l = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    const float y = rcp_ranged(l);
+    o0 = div_shared(v0, l, y); o1 = div_shared(v1, l, y); o2 = div_shared(v2, l, y);
+}
 __device__ __forceinline__ void normalize3(float v0, float v1, float v2, float &o0, float &o1, float &o2) {
     const float l = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
     if (VX_NORM_MK) {               // one IEEE reciprocal, three exact corrections
@@ -749,7 +771,11 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
         const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;   // second
         float w0, w1, w2;
         white(a, unorm, u * kRoughScale, v * kRoughScale, w0, w1, w2);
-        normalize3(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+        // |n + 0.1 w| lies in [0.89, 1.11] (unit axis n, |w_i| <= 1): rcp_ranged is exact
+        if (VX_ROUGH_RCP)
+            normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+        else
+            normalize3(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
     }
     float base0 = 1.0f, base1 = 1.0f, base2 = 1.0f;
     if (g.color < 22) { base0 = kPalette[g.color][0]; base1 = kPalette[g.color][1]; base2 = kPalette[g.color][2]; }
@@ -977,7 +1003,8 @@ void k_render(KernelArgs a) {
     __shared__ float4 s_lds[64 + 128];
     float *s_unorm = reinterpret_cast<float *>(s_lds);
 #pragma unroll
-    for (int i = threadIdx.x; i < 256; i += kWG) s_unorm[i] = (float)i / 255.0f;
+    for (int i = threadIdx.x; i < 256; i += kWG)        // = (float)i / 255.0f, the IEEE quotient (§5)
+        s_unorm[i] = VX_UNORM_MK ? div_const((float)i, 255.0f, 1.0f / 255.0f) : (float)i / 255.0f;
     if (threadIdx.x < 128) {
         const float k = (float)threadIdx.x;
         const SunRay &S0 = a.fc.sun_k[0];
