@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: consecutive frames alternate over this many streams and framebuffers "
+                         "(double buffering), so one frame's launch gap and tail overlap the next (~6%%, "
+                         "profiles/r01_overlap.txt); 1 = one stream")
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed frames rendered before the warmup so the GPU clock leaves its idle state "
                          "(a ~5 ms burst runs ~12%% slower than steady state: profiles/r01_clock_settle.txt)")
@@ -95,30 +99,47 @@ def main():
     samples = args.samples if args.samples is not None else cfg.get("samples", 1)
     frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
                                  sun_radius=args.sun_radius if samples > 1 else 0.0)
-    torch_stream = torch.cuda.Stream()          # a real stream: torch events and the kernels share it
-    torch.cuda.set_stream(torch_stream)
-    stream = torch_stream.cuda_stream
+    # K frames in flight: frame i renders on stream i % K into framebuffer
+    # i % K (a swap chain); real streams, so torch events and kernels share them
+    K = max(1, args.inflight)
+    streams = [torch.cuda.Stream() for _ in range(K)]
+    torch.cuda.set_stream(streams[0])
+    stream = streams[0].cuda_stream
 
     tiles_x, tiles_y = -(-W // TILE), -(-H // TILE)
     n_tiles = tiles_x * tiles_y
     if world == 1:
-        out = torch.empty(H * W * 4, dtype=torch.uint8, device="cuda")
+        outs = [torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") for _ in range(K)]
+        out = outs[0]
 
-        def step():
-            scene.render_device(frame, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+        def make_step(j):
+            o, sj = outs[j], streams[j].cuda_stream
+            return lambda: scene.render_device(frame, o.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)
 
         st = scene.render_device(frame, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
         stats = st.as_dict()
     else:
         from voxmap_amd.dist import ShardedFrame, TileLayout
         layout = TileLayout(W, H, TILE)
-        sharded = ShardedFrame(
-            dist, layout, 4, torch.uint8, "cuda",
-            render_tiles=lambda ids, buf: scene.render_tiles(frame, TILE, ids, buf.data_ptr(),
-                                                             pixel_format=vx.PIXEL_RGBA8, stream=stream),
-            detile=lambda ids, cat, fr: scene.detile(W, H, TILE, ids, cat.data_ptr(), fr.data_ptr(),
-                                                     pixel_format=vx.PIXEL_RGBA8, stream=stream))
-        step = sharded.step
+        shards = []
+        for j in range(K):
+            sj = streams[j].cuda_stream
+            shards.append(ShardedFrame(
+                dist, layout, 4, torch.uint8, "cuda",
+                render_tiles=lambda ids, buf, sj=sj: scene.render_tiles(frame, TILE, ids, buf.data_ptr(),
+                                                                        pixel_format=vx.PIXEL_RGBA8, stream=sj),
+                detile=lambda ids, cat, fr, sj=sj: scene.detile(W, H, TILE, ids, cat.data_ptr(), fr.data_ptr(),
+                                                                pixel_format=vx.PIXEL_RGBA8, stream=sj)))
+
+        def make_step(j):
+            sh, strm = shards[j], streams[j]
+
+            def f():
+                with torch.cuda.stream(strm):      # the gather and de-tile follow this frame's stream
+                    sh.step()
+            return f
+
+        sharded = shards[0]
         st = scene.render_tiles(frame, TILE, layout.rank_tiles(world, rank), sharded.buf.data_ptr(),
                                 pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
         keys = [k for k in st.as_dict().keys() if k != "kernel_ms"]
@@ -126,6 +147,12 @@ def main():
         dist.all_reduce(vec)
         stats = {k: float(v) for k, v in zip(keys, vec.tolist())}
         stats["kernel_ms"] = float(st.kernel_ms)
+    step_fns = [make_step(j) for j in range(K)]
+    n_done = [0]
+
+    def step():
+        step_fns[n_done[0] % K]()
+        n_done[0] += 1
 
     # clock settle: every rank renders the same number of untimed frames (the
     # sharded step holds a collective), sized from a short probe to ~settle_ms
@@ -150,19 +177,28 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
     for _ in range(args.steps):
         step()
-    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1) / args.steps
+    ev_ms = None
+    if world == 1:
+        # per-launch kernel time for the roofline: the same frames on ONE stream,
+        # HIP events on that stream (no overlap; agrees with rocprofv3's average)
+        one = make_step(0)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record()
+        for _ in range(args.steps):
+            one()
+        ev1.record()
+        torch.cuda.synchronize()
+        ev_ms = ev0.elapsed_time(ev1) / args.steps
     t_local = wall
     if world > 1:
         tt = torch.tensor([wall], dtype=torch.float64, device="cuda")
@@ -172,24 +208,32 @@ def main():
 
     v1 = None
     if world == 1 and flags != 0 and args.flags is None and samples <= 1:
-        # the reference's own shader (v1, flags 0) on the same frame, same stream
+        # the reference's own shader (v1, flags 0) on the same frame: the same
+        # K-in-flight wall timing, and one stream with events for its roofline
         fr1 = presets.camera_frame(cam, W, H, scale=up)
         st1 = scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
-        for _ in range(args.warmup):
-            scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+        v1fns = [(lambda o=outs[j], sj=streams[j].cuda_stream:
+                  scene.render_device(fr1, o.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
+        for i in range(args.warmup):
+            v1fns[i % K]()
         torch.cuda.synchronize()
+        tw = time.perf_counter()
+        for i in range(args.steps):
+            v1fns[i % K]()
+        torch.cuda.synchronize()
+        ms1w = 1000.0 * (time.perf_counter() - tw) / args.steps
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.steps):
-            scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream)
+            v1fns[0]()
         e1.record()
         torch.cuda.synchronize()
         ms1 = e0.elapsed_time(e1) / args.steps
         r1 = st1.pixels + st1.shadow_rays
-        v1 = {"ms_per_frame": round(ms1, 4), "mrays_per_s": round(r1 / ms1 / 1e3, 3), "rays_per_frame": int(r1),
-              "alg_bytes": int(st1.alg_bytes), "roofline_frac": round(st1.alg_bytes / (ms1 * 1e-3) / 1e9 /
-                                                                      HBM_PEAK_GBPS, 4)}
+        v1 = {"ms_per_frame": round(ms1w, 4), "mrays_per_s": round(r1 / ms1w / 1e3, 3), "rays_per_frame": int(r1),
+              "single_stream_ms_per_frame": round(ms1, 4), "alg_bytes": int(st1.alg_bytes),
+              "roofline_frac": round(st1.alg_bytes / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
     rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
     value = rays * args.steps / t_local / 1e6                 # whole-job Mrays/s
@@ -236,6 +280,8 @@ def main():
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
                 "tiles": {"size": TILE, "count": n_tiles, "assignment": "round-robin"} if world > 1 else None,
                 "fps": round(1000.0 / ms_per_step, 2),
+                "inflight": {"frames": K, "streams": K, "framebuffers": K,
+                             "single_stream_ms_per_frame": round(ev_ms, 4) if ev_ms is not None else None},
                 "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
                 "shadow_rays": int(stats["shadow_rays"]), "reflect_rays": int(stats["reflect_rays"]),
                 "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / t_local / 1e6, 3),

@@ -423,7 +423,10 @@ int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void
 // in-flight kernel never sees the buffer change under it.
 static int upload_ids(hipStream_t st, const int *ids, int n, int **d_buf, int *cap, std::vector<int> &last) {
     if ((int)last.size() == n && std::equal(last.begin(), last.end(), ids)) return VX_OK;
-    VX_HIP(hipStreamSynchronize(st));
+    // a changed list: every launch that may still read the old one (frames in
+    // flight on other streams included) must finish first
+    (void)st;
+    VX_HIP(hipDeviceSynchronize());
     if (n > *cap) {
         if (*d_buf) VX_HIP(hipFree(*d_buf));
         *d_buf = nullptr;
