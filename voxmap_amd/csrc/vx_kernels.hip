@@ -32,6 +32,9 @@
 #ifndef VX_MARCH_PAD
 #define VX_MARCH_PAD 1
 #endif
+#ifndef VX_MARCH_SG
+#define VX_MARCH_SG 1
+#endif
 #ifndef VX_PAD_MARCH
 #define VX_PAD_MARCH 0
 #endif
@@ -220,6 +223,26 @@ __device__ __forceinline__ float march_len(const SunRay &S, float f0, float f1, 
     return len;
 }
 
+// march_len with the sun's axis signs known at compile time (SG bit i: r_i > 0;
+// the fast paths have no zero component): fract(-f*s) + 1e-4 without the
+// multiply -- for s > 0 it is (-f) - floor(-f) = ceil(f) - f, the same single
+// IEEE subtraction (floor(-f) = -ceil(f)); for s < 0, f - floor(f).
+template <int SG>
+__device__ __forceinline__ float march_len_sg(const SunRay &S, float f0, float f1, float f2) {
+    const float d0 = ((SG & 1) ? ceilf(f0) - f0 : f0 - floorf(f0)) + 1e-4f;
+    const float d1 = ((SG & 2) ? ceilf(f1) - f1 : f1 - floorf(f1)) + 1e-4f;
+    const float d2 = ((SG & 4) ? ceilf(f2) - f2 : f2 - floorf(f2)) + 1e-4f;
+    const float t0 = div_const(d0, S.abs[0], S.rcp[0]);                                // :97
+    const float t1 = div_const(d1, S.abs[1], S.rcp[1]);
+    const float t2 = div_const(d2, S.abs[2], S.rcp[2]);
+    float len = __builtin_fminf(__builtin_fminf(t0, t1), t2);                         // :100-105, one axis
+    if (__builtin_amdgcn_fmed3f(t0, t1, t2) == len) {                                  // ties: literal length
+        const float v0 = t0 == len ? t0 : 0.0f, v1 = t1 == len ? t1 : 0.0f, v2 = t2 == len ? t2 : 0.0f;
+        len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    }
+    return len;
+}
+
 __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
                            float f1, float f2, unsigned &fetches, unsigned &witers) {
     const FrameConsts &F = a.fc;
@@ -267,6 +290,7 @@ __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *
 // same fp32 products r*safe of :118 for every possible safe, indexed by the
 // loaded texel -- one ds_read_b128 instead of three multiplies and the
 // byte -> float convert.  nullptr: multiply in the loop (soft-shadow samples).
+template <int SG>   // -1: signs at run time; else the sun's axis signs (march_len_sg)
 __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
                                           int c2, float f0, float f1, float f2, unsigned &fetches, unsigned &witers,
                                           const float4 *rstep) {
@@ -276,7 +300,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     if (maxs <= 0) return maxs == 0;
     const float xpf = (float)a.SXp;
     float e0 = (float)(c0 + a.SB), e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB);
-    float len = march_len(S, f0, f1, f2);
+    float len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));
     const unsigned sxpyp = a.SXpYp;
     int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
     // one step of :94-128 -> the texel (-1: left the grid)
@@ -305,7 +329,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
         do {
             int t;
             VX_PAD_STEP(t)
-            len = march_len(S, f0, f1, f2);                                      // next step, under the load
+            len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));                                      // next step, under the load
             tv = t;
             witers += once_per_wave(1u);         // counted in the loop: step stays a scalar
         } while (tv > 0 && ++step < maxs - 1);
@@ -367,9 +391,22 @@ __device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_
 __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
                                           float f1, float f2, unsigned &fetches, unsigned &witers,
                                           const float4 *rstep = nullptr) {
-    if (VX_MARCH_PAD && S.fast && a.sunp)
-        return march_pad(a, S, S.up ? a.sunp : a.sunp + a.sunp_texels, c0, c1, c2, f0, f1, f2, fetches, witers,
-                         VX_RSTEP ? rstep : nullptr);
+    if (VX_MARCH_PAD && S.fast && a.sunp) {
+        const int8_t *ch = S.up ? a.sunp : a.sunp + a.sunp_texels;
+        const float4 *rs = VX_RSTEP ? rstep : nullptr;
+#if VX_MARCH_SG
+        // wave-uniform switch on the frame's sun signs: one specialised loop each
+        const int sg = (S.sign[0] > 0.0f ? 1 : 0) | (S.sign[1] > 0.0f ? 2 : 0) | (S.sign[2] > 0.0f ? 4 : 0);
+        switch (sg) {
+#define VX_SG(K) case K: return march_pad<K>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rs);
+            VX_SG(0) VX_SG(1) VX_SG(2) VX_SG(3) VX_SG(4) VX_SG(5) VX_SG(6)
+            default: return march_pad<7>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rs);
+#undef VX_SG
+        }
+#else
+        return march_pad<-1>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rs);
+#endif
+    }
     const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
     return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers)
                   : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers);
