@@ -29,7 +29,7 @@ def _frame():
     return img
 
 
-def _worker(rank, world, port, ts, q):
+def _worker(rank, world, port, ts, q, inflight=1, rounds=1):
     import torch
     import torch.distributed as dist
 
@@ -38,23 +38,35 @@ def _worker(rank, world, port, ts, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        img = _frame()
+        base = _frame()
         layout = TileLayout(100, 70, ts)
-        padded = np.zeros((layout.tiles_y * ts, layout.tiles_x * ts, 4), np.float32)
-        padded[:70, :100] = img
 
-        def render_tiles(ids, buf):
-            for k, t in enumerate(ids):
-                x0, y0 = (t % layout.tiles_x) * ts, (t // layout.tiles_x) * ts
-                buf[k] = torch.from_numpy(padded[y0:y0 + ts, x0:x0 + ts])
+        def context(img):
+            padded = np.zeros((layout.tiles_y * ts, layout.tiles_x * ts, 4), np.float32)
+            padded[:70, :100] = img
 
-        def detile(ids, cat, frame):
-            frame.copy_(torch.from_numpy(detile_host(cat.numpy(), layout, ids)))
+            def render_tiles(ids, buf):
+                for k, t in enumerate(ids):
+                    x0, y0 = (t % layout.tiles_x) * ts, (t // layout.tiles_x) * ts
+                    buf[k] = torch.from_numpy(padded[y0:y0 + ts, x0:x0 + ts])
 
-        sf = ShardedFrame(dist, layout, 4, torch.float32, "cpu", render_tiles, detile)
-        out = sf.step()
+            def detile(ids, cat, frame):
+                frame.copy_(torch.from_numpy(detile_host(cat.numpy(), layout, ids)))
+
+            return ShardedFrame(dist, layout, 4, torch.float32, "cpu", render_tiles, detile)
+
+        # frames in flight (bench.py --inflight): one ShardedFrame per in-flight
+        # frame, each with its own buffers and content, stepped alternately
+        imgs = [base + np.float32(j) for j in range(inflight)]
+        ctxs = [context(im) for im in imgs]
+        ok = True
+        for i in range(rounds * inflight):
+            j = i % inflight
+            out = ctxs[j].step()
+            if rank == 0:
+                ok &= bool(np.array_equal(out.numpy().view(np.uint32), imgs[j].view(np.uint32)))
         if rank == 0:
-            q.put(bool(np.array_equal(out.numpy().view(np.uint32), img.view(np.uint32))))
+            q.put(ok)
     finally:
         dist.destroy_process_group()
 
@@ -66,6 +78,23 @@ def test_sharded_frame_gloo(built, world, ts):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, ts, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+def test_sharded_frames_in_flight_gloo(built):
+    """Two frames in flight (bench.py's double buffering for N > 1): two
+    ShardedFrames stepped alternately keep their own tiles and frames."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 16, q, 2, 3)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
