@@ -35,6 +35,15 @@
 #ifndef VX_MARCH_SG
 #define VX_MARCH_SG 1
 #endif
+#ifndef VX_AO_CVT
+#define VX_AO_CVT 1
+#endif
+#ifndef VX_WRAP_FAST
+#define VX_WRAP_FAST 1
+#endif
+#ifndef VX_AO_DELTA
+#define VX_AO_DELTA 1
+#endif
 #ifndef VX_PAD_MARCH
 #define VX_PAD_MARCH 0
 #endif
@@ -582,7 +591,10 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
     const float u = coord * (float)size - 0.5f;
     const float fl = floorf(u);
     w = u - fl;
-    const int i = f2i(fl);
+    // AO coordinates are finite and far inside +-2^24 ((cell + fract) of a
+    // fragment next to the grid): ivec3()'s NaN / saturation rules never
+    // apply, so a plain convert is f2i here
+    const int i = VX_AO_CVT ? (int)fl : f2i(fl);
     const int j = i + 1;
     i0 = min(max(i, 0), size - 1);
     i1 = min(max(j, 0), size - 1);
@@ -596,9 +608,21 @@ __device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1
     lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
+#if VX_AO_DELTA
+    // one byte offset and three deltas (0 or one row / plane / cell: the
+    // clamped corners differ by at most one cell per axis)
+    const unsigned b000 = lin_index(a, x0, y0, z0) << 1;
+    const unsigned dx = (unsigned)(x1 - x0) << 1, dy = __umul24((unsigned)(y1 - y0), 2u * (unsigned)a.X),
+                   dz = __umul24((unsigned)(z1 - z0), 2u * a.XY);
+    const unsigned b010 = b000 + dy, b001 = b000 + dz, b011 = b010 + dz;
+    auto ld = [&](unsigned off) -> uint32_t { return (uint32_t)ld_off(a.rg, off); };
+    const uint32_t t000 = ld(b000), t100 = ld(b000 + dx), t010 = ld(b010), t110 = ld(b010 + dx);
+    const uint32_t t001 = ld(b001), t101 = ld(b001 + dx), t011 = ld(b011), t111 = ld(b011 + dx);
+#else
     auto ld = [&](int x, int y, int z) -> uint32_t { return (uint32_t)ld_off(a.rg, lin_index(a, x, y, z) << 1); };
     const uint32_t t000 = ld(x0, y0, z0), t100 = ld(x1, y0, z0), t010 = ld(x0, y1, z0), t110 = ld(x1, y1, z0);
     const uint32_t t001 = ld(x0, y0, z1), t101 = ld(x1, y0, z1), t011 = ld(x0, y1, z1), t111 = ld(x1, y1, z1);
+#endif
     float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
@@ -618,7 +642,21 @@ __device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1
 // floor(fl / n) with the IEEE quotient by n = 2^k, which is exactly fl * 2^-k
 // (fl is 0 or |fl| >= 1: no underflow), so the multiply by rn = 1/n (exact,
 // host-side) replaces a ~10-instruction correctly rounded division.
+// |fl| < 2^24 (every cloud lookup; a mountain lookup unless r1 ~ 0): fl - q*n
+// is exact and in [0, n), i.e. (int)fl mod n = (int)fl & (n - 1); the literal
+// form only for the lanes outside that range (NaN included).
 __device__ __forceinline__ int wrap_idx(float fl, int n, float rn) {
+    if (VX_WRAP_FAST) {
+        int r = (int)fl & (n - 1);
+        if (!(fabsf(fl) < 16777216.0f)) {
+            // 1/n from n (exact: a power of two), not from a kernel argument:
+            // a load sunk into this rare block would be tail-merged across the
+            // u/v calls into a pointer phi -- a KernelArgs copy to scratch
+            const float q = floorf(fl * (1.0f / (float)n));
+            r = f2i(fl - q * (float)n) & (n - 1);
+        }
+        return r;
+    }
     const float q = floorf(fl * rn);
     return f2i(fl - q * (float)n) & (n - 1);
 }
