@@ -92,6 +92,26 @@ def test_field_octant_copies_match_oracle(noise, octant):
     assert np.array_equal(box[..., 1:], oracle.field_box(field, octant, 32))
 
 
+@pytest.mark.parametrize("octant", [0, 3, 5])
+def test_box_extents_full_scene_match_oracle(octant):
+    """Device traversal boxes (k_oct_box: prefix sums + bisection) == the
+    oracle's vxo_field_box on the BASELINE 1024x256x32 field, and min(e) is
+    the octant's air cube (vxo_field_octant)."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid("s_proc")
+    Z, Y, X = grid.shape
+    with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, dims=(X, Y, Z), device=0) as sc:
+        field = sc.read_field(0)
+        box = sc.read_boxes(octant)
+    r = oracle.field_octant(field, octant, 32)
+    e = oracle.field_box(field, octant, 32, r_cube=r)
+    assert np.array_equal(box[..., 0], field[..., 2])
+    assert np.array_equal(box[..., 1:], e)
+    assert np.array_equal(e.min(axis=3), r)
+
+
 @pytest.fixture(scope="module")
 def full_scene(noise):
     import voxmap_amd as vx
