@@ -40,8 +40,22 @@ extern "C" {
 #define VX_FORMAT_BIN 1     /* raw RGBA8 bytes */
 #define VX_FORMAT_BIN_GZ 2  /* gzip of raw (makefile:70-71) */
 #define VX_FORMAT_BLOB 3    /* AES-256-CBC(PKCS#7, fixed IV) of gzip (encrypt.js:12-46) */
-#define VX_FORMAT_GRID 4    /* map only: raw palette-index grid, X*Y*Z bytes (the input of
-                               sdf.cpp); the distance field is built on the GPU */
+#define VX_FORMAT_GRID 4    /* map only: raw palette-index grid, X*Y*Z bytes, 0 = air (the
+                               input of sdf.cpp after its remap); the distance field is
+                               built on the GPU */
+
+/* Palette (render.vert:20-22): sdf.cpp builds it as {0 = air} + the map's
+ * colours in ascending order (sdf.cpp:188-227), glass sorting last, so the
+ * shipped shader has pal_size = 22 entries and glass = pal_size - 1 = 21.
+ * map.bin's B channel is the remapped index, and the remap (sdf.cpp:229-233)
+ * turns AIR into pal_size (the first zero entry of the zero-initialised pal[]).
+ * The mesh (sdf.cpp:284) has faces only for colours < pal_size, and colour 0
+ * never survives the remap: a cell is a surface candidate ("meshed") iff
+ * 1 <= B <= VX_PAL_SIZE - 1.  Every other B -- air written as 22 by sdf.cpp,
+ * 0 in palette grids (VX_FORMAT_GRID) -- is never a surface.  Shadows and AO
+ * read R/G only: a block is R == G == 0 (sdf.cpp:430). */
+#define VX_PAL_SIZE 22
+#define VX_GLASS (VX_PAL_SIZE - 1)
 
 /* output pixel formats */
 #define VX_PIXEL_RGBA32F 0  /* 16 B/pixel, parity format */
@@ -182,8 +196,10 @@ int vx_decode(const void *in, size_t n, int format, const char *key_jwk_k,
 int vx_blob_encrypt(const void *in, size_t n, const char *key_jwk_k,
                     void *out, size_t out_cap, size_t *out_size);
 
-/* map.bin from a palette-index grid (x fastest): sdf.cpp:405-470.
- * rgba_out holds X*Y*Z*4 bytes; A is written 0 as sdf.cpp:469 does. */
+/* map.bin from a palette-index grid (x fastest, 0 = air, 1..21 palette
+ * indices): sdf.cpp:405-470.  rgba_out holds X*Y*Z*4 bytes: R = up radius,
+ * G = down radius, B = the index with air written as VX_PAL_SIZE (sdf.cpp:
+ * 229-233, 466-468), A = 0 (sdf.cpp:469). */
 int vx_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int n_threads);
 
 /* Same output as vx_field_build, computed on GPU `device` (plane-parallel

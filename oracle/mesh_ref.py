@@ -12,7 +12,11 @@ traversal against.
 Restated (read as text, not copied):
   * ccol(x, y, z): palette index with clamped coordinates (sdf.cpp:44-51), so
     the grid boundary has no faces;
-  * for every colour c (0 = air included, sdf.cpp:284), every chunk of
+  * cells hold map.bin's B: the remapped palette index, with AIR written as
+    pal_size (sdf.cpp:19,188,229-233: pal[] is zero-initialised and scanned
+    from 1, so air finds pal[pal_size] = 0);
+  * for every colour c < pal_size (sdf.cpp:284: colour 0 never occurs after
+    the remap and air = pal_size is never meshed), every chunk of
     CHUNK = Z cells per axis (voxmap.h:9, :62-67), every axis d and normal
     0/1, slices p[d] = -1 .. CHUNK-1 (sdf.cpp:299-311): mask = (normal 0:
     cell of colour c, cell ahead not) or (normal 1: cell not c, cell ahead c);
@@ -40,12 +44,19 @@ import numpy as np
 GLASS = 21  # pal_size - 1 (sdf.cpp:225, :337)
 
 
+def remap_air(grid_zyx: np.ndarray, pal_size: int = 22) -> np.ndarray:
+    """Palette grid (0 = air) -> map.bin's B channel: air becomes pal_size (sdf.cpp:229-233)."""
+    g = np.asarray(grid_zyx)
+    return np.where(g == 0, pal_size, g).astype(g.dtype)
+
+
 def greedy_mesh(grid_zyx: np.ndarray, pal_size: int = 22) -> np.ndarray:
-    """Quads of sdf.cpp:281-356 for a (Z, Y, X) palette grid.
+    """Quads of sdf.cpp:281-356 for a (Z, Y, X) palette grid (0 = air, remapped
+    to pal_size first, as sdf.cpp does before meshing).
 
     Returns an int32 array (n, 12): x, y, z, du(3), dv(3), colour, normal, id.
     """
-    g = np.asarray(grid_zyx)
+    g = remap_air(grid_zyx, pal_size)
     Z, Y, X = g.shape
     col = np.ascontiguousarray(np.transpose(g, (2, 1, 0)))   # col[x][y][z] as the reference indexes
     dims = (X, Y, Z)
@@ -53,7 +64,7 @@ def greedy_mesh(grid_zyx: np.ndarray, pal_size: int = 22) -> np.ndarray:
     quads = []
     for color in range(pal_size):
         is_c = col == color
-        if not is_c.any() and color != 0:
+        if not is_c.any():         # colour 0 (and unused colours): no quads
             continue
         for cx in range(0, X, CH):
             for cy in range(0, Y, CH):
@@ -170,3 +181,81 @@ def cast(quads: np.ndarray, origin, dirs: np.ndarray):
             out[key_e][s:s + chunk] = np.where(ok, e.min(axis=1), np.inf)
         out["n_glass"][s:s + chunk] = ng
     return out
+
+
+# ---- 2D mode mesh (sdf.cpp:362-401) and the vertex record layout ------------------
+# The plaintext res/vertex2d.bin.gz is the one reference OUTPUT of the mesher that
+# ships unencrypted.  Regenerating it byte for byte from the footprint it encodes
+# pins the greedy merge order, the quad/triangle/record layout and the rule that
+# air (c2d = pal_size after the remap, sdf.cpp:235-239) is never meshed.
+
+REC2D = np.dtype([("p", "<i2", 3), ("d", "<i2", 3), ("c", "u1"), ("n", "u1"), ("id", "u1"), ("pad", "u1")])
+
+
+def decode_vertex2d(raw: bytes, dims=(1024, 256), pal_size: int = 22) -> np.ndarray:
+    """c2d[x][y] (X, Y) from vertex2d.bin bytes: each 6-vertex quad covers
+    [x, x + w) x [y, y + h) with its colour; cells no quad covers are air
+    (pal_size after the remap, sdf.cpp:235-239)."""
+    rec = np.frombuffer(raw, REC2D)
+    assert len(rec) % 6 == 0
+    X, Y = dims
+    c2d = np.full((X, Y), pal_size, np.int32)
+    for q in rec.reshape(-1, 6):
+        x, y = int(q[0]["p"][0]), int(q[0]["p"][1])
+        w, h = int(q["d"][:, 0].max()), int(q["d"][:, 1].max())
+        c2d[x:x + w, y:y + h] = int(q[0]["c"])
+    return c2d
+
+
+def mesh2d(c2d: np.ndarray, pal_size: int = 22) -> list:
+    """Quads (x, y, w, h, colour, id) of sdf.cpp:367-397: per colour c < pal_size,
+    cells visited x-major then y (forXY, voxmap.h:45-49); a quad grows along x
+    while the mask holds (:378), then along y while the whole row of w cells
+    holds (:380-385); its cells are cleared (:391-395); id 2 for glass =
+    pal_size - 1 (:388)."""
+    X, Y = c2d.shape
+    quads = []
+    for color in range(pal_size):
+        mask = c2d == color
+        if not mask.any():
+            continue
+        for x, y in np.argwhere(mask):          # row-major over (x, y) = forXY order
+            x, y = int(x), int(y)
+            if not mask[x, y]:
+                continue
+            w = 1
+            while x + w < X and mask[x + w, y]:
+                w += 1
+            h = 1
+            while y + h < Y and mask[x:x + w, y + h].all():
+                h += 1
+            quads.append((x, y, w, h, color, 2 if color == pal_size - 1 else 0))
+            mask[x:x + w, y:y + h] = False
+    return quads
+
+
+def vertex2d_bytes(quads) -> bytes:
+    """vert2d records (sdf.cpp:154-162: i16 x, y, 0, dx, dy, 0, u8 colour, 0, id, 0)
+    of quad2d(x, y, w, 0, 0, h) = tri2d((0,0), (w,0), (0,h)) + tri2d((0,h), (w,0),
+    (w,h)) (sdf.cpp:163-173, :389)."""
+    out = np.zeros(6 * len(quads), REC2D)
+    for k, (x, y, w, h, c, i) in enumerate(quads):
+        for j, (dx, dy) in enumerate(((0, 0), (w, 0), (0, h), (0, h), (w, 0), (w, h))):
+            out[6 * k + j] = ((x, y, 0), (dx, dy, 0), c, 0, i, 0)
+    return out.tobytes()
+
+
+def vertex_bytes(quads: np.ndarray) -> bytes:
+    """vert records of the 3D mesh (sdf.cpp:94-141): quad() = tri(0, du, dv) +
+    tri(dv, du, du + dv), each tri's last two vertices swapped for odd normals
+    (:112-118, the winding GL culls by)."""
+    rec = np.dtype([("p", "<i2", 3), ("d", "<i2", 3), ("c", "u1"), ("n", "u1"), ("id", "u1"), ("pad", "u1")])
+    out = []
+    for q in np.asarray(quads):
+        o, du, dv = q[0:3], q[3:6], q[6:9]
+        c, n, i = int(q[9]), int(q[10]), int(q[11])
+        for a, b, cc in ((0 * du, du, dv), (dv, du, du + dv)):
+            tri = (a, cc, b) if n % 2 else (a, b, cc)
+            for d in tri:
+                out.append(((int(o[0]), int(o[1]), int(o[2])), tuple(int(v) for v in d), c, n, i, 0))
+    return np.array(out, rec).tobytes()

@@ -8,11 +8,14 @@ loop-for-loop transliteration, so only small dims finish quickly):
   summed volume table, forXYZ .......... sdf.cpp:407-422
   half-cube radii with the mid shortcut  sdf.cpp:429-457
   map.bin texel order (R, G, B=col, A=0) sdf.cpp:462-470
+  air remapped to B = pal_size ......... sdf.cpp:19,188,229-233
 Arrays are zero-initialised like the reference's globals (sdf.cpp:22-25).
 """
 from __future__ import annotations
 
 import numpy as np
+
+PAL_SIZE = 22   # render.vert:21 palette entries: 0 (air) + 20 colours + glass
 
 
 def build(color_zyx: np.ndarray) -> np.ndarray:
@@ -64,5 +67,8 @@ def build(color_zyx: np.ndarray) -> np.ndarray:
     for z in range(Z):
         for y in range(Y):
             for x in range(X):
-                out[z, y, x] = (sdf[x][y][z][0] & 0xFF, sdf[x][y][z][1] & 0xFF, col[x][y][z] & 0xFF, 0)
+                # B = the remapped index: air (0) finds pal[pal_size] = 0 in the
+                # zero-initialised pal[] scanned from 1 (sdf.cpp:19,188,229-233)
+                b = col[x][y][z] if col[x][y][z] else PAL_SIZE
+                out[z, y, x] = (sdf[x][y][z][0] & 0xFF, sdf[x][y][z][1] & 0xFF, b & 0xFF, 0)
     return out

@@ -125,6 +125,15 @@ void vxo_palette(float out[22][3]);
 /* Deterministic transcendental used by both oracle and kernel. */
 float vxo_exp2(float x);
 
+/* --- palette / air encoding ---------------------------------------------
+ * sdf.cpp builds the palette as {0} + the map's colours (sdf.cpp:188-227):
+ * pal_size = 22 for the shipped shader (render.vert:21), glass = 21.  The
+ * remap (sdf.cpp:229-233) writes air as B = pal_size; the mesher meshes only
+ * colours < pal_size (sdf.cpp:284) and colour 0 never survives the remap.  So
+ * a cell can show a face iff 1 <= B <= 21 ("vis colour" B, else 0). */
+#define VXO_PAL_SIZE 22
+static inline int vxo_vis(int b) { return (b >= 1 && b < VXO_PAL_SIZE) ? b : 0; }
+
 /* --- field (map.bin) definition, vxo_field.c ---------------------------- */
 /* Build the RGBA8 field from a palette-index grid (x fastest), restating
  * sdf.cpp:405-470 literally (serial x->y->z order, clamped-index quirks). */

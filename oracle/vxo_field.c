@@ -13,7 +13,8 @@
  *     [mid-1, mid+1] (sdf.cpp:439-444), which makes the serial x->y->z order
  *     (voxmap.h:50-55) part of the definition;
  *   - blocks keep sdf = 0; map.bin is written z->y->x as R,G,B=col,A=0
- *     (sdf.cpp:462-470).
+ *     (sdf.cpp:462-470), with air remapped to B = pal_size = 22
+ *     (sdf.cpp:19,188,229-233).
  * The reference C++ itself is NOT compiled (SURVEY.md §8c permission denial);
  * this is a from-text restatement.
  *
@@ -91,11 +92,15 @@ void vxo_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba) {
                     c.sdf[2 * IDX(&c, x, y, z) + o] = (unsigned char)r;
                 }
             }
-    /* map.bin texels (sdf.cpp:462-470) */
+    /* map.bin texels (sdf.cpp:462-470).  B is the remapped palette index:
+     * sdf.cpp:229-233 scans pal[i] from i = 1 for the cell's colour; pal[]
+     * is zero-initialised (sdf.cpp:19) and pal[0] = 0 is air (sdf.cpp:188),
+     * so air finds the first zero entry past the palette, pal[pal_size]:
+     * air is written as B = pal_size = VXO_PAL_SIZE. */
     for (size_t i = 0; i < N; i++) {
         rgba[4 * i + 0] = c.sdf[2 * i + 0];
         rgba[4 * i + 1] = c.sdf[2 * i + 1];
-        rgba[4 * i + 2] = color[i];
+        rgba[4 * i + 2] = color[i] ? color[i] : (uint8_t)VXO_PAL_SIZE;
         rgba[4 * i + 3] = 0;
     }
     free(c.sum);
@@ -105,8 +110,8 @@ void vxo_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba) {
 /* Octant box half-size: for octant o (bit 0: x negative,
  * bit 1: y, bit 2: z; a zero direction component counts as positive) the
  * largest L <= cap such that the cube of side L with corner c extending toward
- * the octant holds no non-air cell (B != 0) of the grid; r = L - 1 (0 for
- * non-air cells).  L = min over forward non-air q of max_i (q_i - c_i) s_i,
+ * the octant holds no meshed cell (vxo_vis(B) != 0: no face can be entered
+ * there) of the grid; r = L - 1 (0 for meshed cells).  L = min over forward non-air q of max_i (q_i - c_i) s_i,
  * separable: L = min_dz max(dz, min_dy max(dy, min_dx dx)) over dx, dy, dz in
  * [0, cap).  Cells outside the grid count as air. */
 void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, uint8_t *r_out) {
@@ -122,7 +127,7 @@ void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct
                 for (int k = 0; k < cap; k++) {
                     const int xx = x + k * sx;
                     if (xx < 0 || xx >= X) break;
-                    if (rgba[4 * I3(xx, y, z) + 2]) { best = k; break; }
+                    if (vxo_vis(rgba[4 * I3(xx, y, z) + 2])) { best = k; break; }
                 }
                 g1[I3(x, y, z)] = (unsigned char)best;
             }
@@ -158,7 +163,7 @@ void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct
 }
 
 /* ---- vxo_field_box: the cube r grown to per-axis extents ----
- * Solid = non-air (colour byte != 0); cells outside the grid count as air.
+ * Solid = meshed (vxo_vis(B) != 0); cells outside the grid count as air.
  * ex = max e in [r, cap-1] with box (e, r, r) empty, then ey with (ex, e, r),
  * then ez with (ex, ey, e).  Emptiness is monotone in each extent, so the
  * maximum is found by bisection (the kernel's k_oct_box does the same). */
@@ -191,7 +196,7 @@ void vxo_field_box(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, c
         for (int y = 1; y <= Y; y++)
             for (int x = 1; x <= X; x++) {
                 const size_t c = (size_t)(x - 1) + (size_t)X * ((size_t)(y - 1) + (size_t)Y * (size_t)(z - 1));
-                S[PS(&b, x, y, z)] = (rgba[4 * c + 2] != 0) + S[PS(&b, x - 1, y, z)] + S[PS(&b, x, y - 1, z)] +
+                S[PS(&b, x, y, z)] = (vxo_vis(rgba[4 * c + 2]) != 0) + S[PS(&b, x - 1, y, z)] + S[PS(&b, x, y - 1, z)] +
                                      S[PS(&b, x, y, z - 1)] - S[PS(&b, x - 1, y - 1, z)] - S[PS(&b, x - 1, y, z - 1)] -
                                      S[PS(&b, x, y - 1, z - 1)] + S[PS(&b, x - 1, y - 1, z - 1)];
             }
@@ -202,7 +207,7 @@ void vxo_field_box(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, c
             for (int x = 0; x < X; x++) {
                 const size_t c = (size_t)x + (size_t)X * ((size_t)y + (size_t)Y * (size_t)z);
                 int e[3] = {0, 0, 0};
-                if (rgba[4 * c + 2] == 0) {
+                if (vxo_vis(rgba[4 * c + 2]) == 0) {
                     const int r = r_cube[c];
                     e[0] = e[1] = e[2] = r;
                     for (int a = 0; a < 3; a++) {

@@ -246,15 +246,20 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
 }
 
 /* ---------------- primary visibility ----------------
- * The reference rasterises the greedy mesh of sdf.cpp:281-356.  That mesh has a
- * face wherever two grid-adjacent cells differ in palette index (index 0 = air
- * included, ccol() clamps at the grid edge so the grid boundary has no faces),
- * oriented from the differing cell into the cell of the face's colour, and GL
- * culls back faces (render.js:88-91).  So the visible opaque surface at a pixel
- * is the first in-grid cell boundary along the view ray where the colour
- * changes; the entered cell gives colour and id.  Glass (index 21) is drawn
- * last and blended (render.js:84-86); the surface behind a glass entry is the
- * next colour change, which is never glass, so one blend layer is exact.
+ * The reference rasterises the greedy mesh of sdf.cpp:281-356.  For each
+ * colour c < pal_size (sdf.cpp:284) it has a face wherever a cell of colour c
+ * borders a cell of another colour, oriented out of the c cell (ccol() clamps
+ * at the grid edge, so the grid boundary has no faces), and GL culls back
+ * faces (render.js:88-91).  Air is remapped to B = pal_size (sdf.cpp:19,188,
+ * 229-233) and so is never meshed.  The visible surface at a pixel is
+ * therefore the first step along the view ray that ENTERS a meshed cell
+ * (vxo_vis(B) != 0) from a cell of another colour; the entered cell gives
+ * colour and id.  Glass (index 21) is drawn last and blended
+ * (render.js:84-86): leaving glass into air is no face, so glass blends over
+ * the next entry behind it.  Several glass layers blend in mesh order in the
+ * reference (order-dependent); the build defines one layer: later glass
+ * entries are skipped (the reference's result when the nearer pane is drawn
+ * first and its depth write hides the farther one).
  *
  * Traversal ("box-exit" stepping): from the current cell c, the ray's octant
  * (direction signs s, zero counted positive) has the all-air cube
@@ -296,7 +301,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
         const uint8_t *p_ = octe + 3 * ((size_t)(a)[0] + (size_t)s->X * ((size_t)(a)[1] + (size_t)s->Y * (size_t)(a)[2])); \
         (e)[0] = p_[0]; (e)[1] = p_[1]; (e)[2] = p_[2];                                              \
     } while (0)
-    int prev = tx[2];
+    int prev = vxo_vis(tx[2]);
     int E[3];
     OCT_E(abs_c, E);
     int nrec = 0;
@@ -320,9 +325,13 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
         if (!in_grid(s, abs_c)) return nrec;   /* left the grid: sky behind */
         tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
         (*fetches)++;
-        const int col = tx[2];
+        const int col = vxo_vis(tx[2]);
         OCT_E(abs_c, E);                           /* air box ahead */
-        if (col != prev) {
+        /* a front face: entering a meshed cell from a cell of another colour
+         * (air is never meshed, sdf.cpp:229-233,284); with glass_layer the
+         * first glass entry is recorded and the walk goes on, later glass
+         * entries are not surfaces (one blend layer) */
+        if (col != prev && col != 0 && !(glass_layer && col == GLASS_INDEX && nrec == 1)) {
             vxo_gbuf *h = &g[nrec];
             h->color = col;
             h->id = col == GLASS_INDEX ? 2 : 0;
@@ -338,7 +347,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
                 }
             }
             nrec++;
-            if (!glass_layer || h->id != 2 || nrec == 2) return nrec;
+            if (!glass_layer || h->id != 2) return nrec;
         }
         prev = col;
     }

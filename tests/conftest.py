@@ -25,5 +25,10 @@ def built():
 
 @pytest.fixture(scope="session")
 def noise(built):
+    """The reference's own noise texture (res/noise.bin.gz, shipped in
+    voxmap_amd/data), decoded through the product codec."""
+    import numpy as np
     import voxmap_amd as vx
-    return vx.noise_synth(0)
+    from voxmap_amd import scenes
+    raw = vx.decode(open(scenes.NOISE_PATH, "rb").read(), vx.FORMAT_BIN_GZ)
+    return np.frombuffer(raw, np.uint8).reshape(1024, 1024, 4).copy()

@@ -38,12 +38,9 @@ def test_error_paths_do_not_touch_the_gpu(built):
     with pytest.raises(vx.VoxmapError) as e:
         vx.Scene(map_bytes=b"\x00" * 256, map_format=vx.FORMAT_BIN, dims=(4, 4, 4), dist_cap=300)
     assert e.value.code == -1
-    with pytest.raises(vx.VoxmapError) as e:   # palette index 255 = the traversal's border sentinel
-        vx.Scene(map_bytes=bytes([0, 0, 255, 0]) * 64, map_format=vx.FORMAT_BIN, dims=(4, 4, 4))
-    assert e.value.code == -1 and "reserved" in str(e.value)
     with pytest.raises(vx.VoxmapError) as e:
-        vx.Scene(map_bytes=b"\xff" * 64, map_format=vx.FORMAT_GRID, dims=(4, 4, 4))
-    assert e.value.code == -1
+        vx.Scene(map_bytes=b"\xff" * 63, map_format=vx.FORMAT_GRID, dims=(4, 4, 4))
+    assert e.value.code == -5
     with pytest.raises(vx.VoxmapError) as e:
         vx.decode(b"\x1f\x8bnot really gzip", vx.FORMAT_BIN_GZ)
     assert e.value.code == -3
@@ -144,6 +141,8 @@ def test_field_build_full_size_matches_oracle(built):
     assert a.shape == (32, 256, 1024, 4) and a.nbytes == 33554432     # map.bin size pin
     assert np.array_equal(a, oracle.field_build(g))
     assert not a[..., 3].any()                                           # sdf.cpp:469 writes A = 0
+    assert (a[..., 2][g == 0] == 22).all()                               # air remapped to pal_size (:229-233)
+    assert np.array_equal(a[..., 2][g != 0], g[g != 0])
 
 
 def test_field_semantics_up_down():

@@ -1,6 +1,7 @@
 """The C++ host (voxmap_amd/vxrender, csrc/vx_cli.cpp) over the C ABI: it must
 produce the same RGBA8 frame as the Python mirror for the same scene and
-camera, from a palette grid and from an encrypted .blob."""
+camera, from a palette grid and from an encrypted .blob (air written as B = 22
+the way sdf.cpp writes map.bin, or as 0: identical frames)."""
 import gzip
 import json
 import os
@@ -26,7 +27,7 @@ def test_cli_help_and_errors(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("source", ["grid", "blob"])
+@pytest.mark.parametrize("source", ["grid", "blob", "blob_air0"])
 def test_cli_frame_equals_python_host(built, tmp_path, source):
     import torch
     if not torch.cuda.is_available():
@@ -42,7 +43,9 @@ def test_cli_frame_equals_python_host(built, tmp_path, source):
         path.write_bytes(grid.tobytes())
         extra = ["--format", "grid"]
     else:
-        field = vx.field_build(grid)
+        field = vx.field_build(grid)                 # air = B 22 (sdf.cpp:229-233)
+        if source == "blob_air0":                    # the same map with air written as 0
+            field[..., 2][grid == 0] = 0
         path = tmp_path / "map.blob"
         path.write_bytes(vx.blob_encrypt(gzip.compress(field.tobytes()), KEY))
         extra = ["--key", KEY]

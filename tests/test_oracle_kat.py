@@ -229,6 +229,10 @@ def test_primary_hits_top_face_analytically(O):
 
 
 def test_primary_glass_then_behind_and_boundary_rule(O):
+    """sdf.cpp remaps air to B = pal_size = 22 (sdf.cpp:19,188,229-233) and
+    meshes only colours < pal_size (:284): air is never a surface, the glass
+    pane's far side is a back face (culled, render.js:88-91), so the wall
+    behind the pane is what the glass blends over."""
     import voxmap_amd as vx
     g = np.zeros((8, 16, 32), np.uint8)
     g[0] = 2
@@ -236,18 +240,65 @@ def test_primary_glass_then_behind_and_boundary_rule(O):
     g[1:4, 12, 10:20] = 7          # a wall behind it (y = 12)
     g[1:6, 0:16, 31] = 9           # a wall on the grid's x = 31 edge
     field = _field(g)
+    assert (field[g == 0][:, 2] == 22).all()          # map.bin air is B = pal_size
     o = O.Oracle(field, np.zeros((4, 4, 4), np.uint8))
     fr = vx.make_frame((15.0, 4.0, 2.0), (math.pi / 2, 0.0, 0.0), 16, 16)   # looking +y, level
     d = np.array([0.0, 1.0, 0.01])
     n, gb, _, cap = o.primary(fr.params, d)
     assert n == 2 and gb[0].id == 2 and gb[0].color == 21 and gb[0].normal_idx == 3   # -y face of the pane
-    assert gb[1].color == 0 and gb[1].id == 0   # exiting glass into air: the air face (palette 0) is the surface
-    # entering the grid through its x = 31 edge straight into a block: no face there (ccol clamps),
-    # the first face is where the block ends
+    assert list(gb[0].cell)[1] == 8
+    # behind the pane: the wall's -y face at y = 12 (glass -> air is no face)
+    assert gb[1].color == 7 and gb[1].id == 0 and gb[1].normal_idx == 3 and gb[1].cell[1] == 12
+    # entering the grid through its x = 31 edge straight into a block: no face there (ccol clamps);
+    # leaving the block into air is its back face (culled) and air has none: sky
     fr2 = vx.make_frame((40.0, 5.5, 2.0), (math.pi / 2, 0.0, math.pi / 2), 16, 16)
     d2 = np.array([-1.0, 0.001, 0.002])
     n2, gb2, _, _ = o.primary(fr2.params, d2)
-    assert n2 == 1 and gb2[0].color == 0 and gb2[0].normal_idx == 0 and gb2[0].cell[0] == 31
+    assert n2 == 0
+    # two panes: single blend layer, the second pane is skipped, the wall is behind
+    g2 = g.copy()
+    g2[1:4, 10, 10:20] = 21
+    o2 = O.Oracle(_field(g2), np.zeros((4, 4, 4), np.uint8))
+    n3, gb3, _, _ = o2.primary(fr.params, d)
+    assert n3 == 2 and gb3[0].color == 21 and gb3[0].cell[1] == 8 and gb3[1].color == 7 and gb3[1].cell[1] == 12
+    # glass directly against the wall: the wall's face toward the glass is the surface behind
+    g3 = g.copy()
+    g3[1:4, 9:12, 10:20] = 21
+    o3 = O.Oracle(_field(g3), np.zeros((4, 4, 4), np.uint8))
+    n4, gb4, _, _ = o3.primary(fr.params, d)
+    assert n4 == 2 and gb4[1].color == 7 and gb4[1].cell[1] == 12
+
+
+def test_air_encoding_b22_equals_b0_and_unmeshed_colours(O):
+    """The same scene with air written as B = 22 (sdf.cpp) and as B = 0 (a
+    pre-remap grid) renders identically, with identical work counters.  A
+    block whose B is not a meshed index (>= pal_size, e.g. a black map colour
+    that sdf.cpp remaps to pal_size) shows no face but still casts shadows
+    (R = G = 0)."""
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    g = scenes.small_proc(23, dims=(64, 40, 16), n_boxes=12, n_glass=6)
+    f22 = _field(g)
+    f0 = f22.copy()
+    f0[..., 2][g == 0] = 0
+    noise = vx.noise_synth(0)
+    fr = vx.make_frame((32.0, 20.0, 18.0), (1.1, 0.0, 0.6), 80, 60)
+    a, sa = O.Oracle(f22, noise).render(fr.params, 80, 60)
+    b, sb = O.Oracle(f0, noise).render(fr.params, 80, 60)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa.as_dict() == sb.as_dict()
+    # unmeshed block: invisible, but its R = G = 0 stops the sun march
+    g4 = np.zeros((8, 16, 16), np.uint8)
+    g4[0] = 2
+    g4[3, 8, 8] = 5
+    f4 = _field(g4)
+    f4[3, 8, 8, 2] = 22
+    o4 = O.Oracle(f4, noise)
+    n, gb, _, _ = o4.primary(vx.make_frame((8.5, 8.5, 7.0), (1e-4, 0.0, 0.0), 8, 8).params, (0.0, 0.0, -1.0))
+    assert n == 1 and gb[0].color == 2 and gb[0].cell[2] == 1        # straight through to the ground
+    sun = np.array([0.1, 0.05, 0.99]) / np.linalg.norm([0.1, 0.05, 0.99])
+    m = o4.march((8, 8, 1), (0.5, 0.5, 0.0), tuple(float(f32(v)) for v in sun), 16)
+    assert m.step < 16                                                 # the march stops on the block
 
 
 def test_field_octant_is_air_cube_ahead(O):

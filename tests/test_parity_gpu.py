@@ -34,6 +34,11 @@ def _scene(vx, field, noise, dims):
                     noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0)
 
 
+def _vis(b):
+    """The traversal's colour: meshed palette indices 1..21 (sdf.cpp:284), else 0 (include/voxmap.h)."""
+    return np.where((b >= 1) & (b <= 21), b, 0).astype(np.uint8)
+
+
 def _diff(a, b):
     return int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32)))
 
@@ -88,7 +93,7 @@ def test_field_octant_copies_match_oracle(noise, octant):
         box = sc.read_boxes(octant)
     assert np.array_equal(dev[..., :3], field[..., :3])
     assert np.array_equal(dev[..., 3], oracle.field_octant(field, octant, 32))
-    assert np.array_equal(box[..., 0], field[..., 2])
+    assert np.array_equal(box[..., 0], _vis(field[..., 2]))
     assert np.array_equal(box[..., 1:], oracle.field_box(field, octant, 32))
 
 
@@ -107,7 +112,7 @@ def test_box_extents_full_scene_match_oracle(octant):
         box = sc.read_boxes(octant)
     r = oracle.field_octant(field, octant, 32)
     e = oracle.field_box(field, octant, 32, r_cube=r)
-    assert np.array_equal(box[..., 0], field[..., 2])
+    assert np.array_equal(box[..., 0], _vis(field[..., 2]))
     assert np.array_equal(box[..., 1:], e)
     assert np.array_equal(e.min(axis=3), r)
 
@@ -351,3 +356,53 @@ def test_c5_rows_soft_shadows_full_quality(noise):
     rows = np.arange(step // 2, c["h"], step)
     _compare(img, ref, rows)
     assert st.primary_cap_hits == 0
+
+
+# ---- the reference's map.bin air encoding ------------------
+def test_air_b22_and_b0_render_identically(noise, tmp_path):
+    """map.bin from sdf.cpp writes air as B = pal_size = 22 (sdf.cpp:229-233,
+    466-468); a pre-remap grid has 0.  Both must give identical frames and
+    identical work counters (primary fetches: the traversal boxes ignore the
+    encoding) -- through FORMAT_BIN here and through a .blob in vxrender
+    (tests/test_cli.py) -- and equal the oracle."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (128, 64, 24)
+    grid = scenes.small_proc(11, dims=dims, n_boxes=16, n_glass=12)
+    f22 = vx.field_build(grid)
+    assert (f22[..., 2][grid == 0] == 22).all()
+    f0 = f22.copy()
+    f0[..., 2][grid == 0] = 0
+    fr = vx.make_frame((64.0, 32.0, 14.0), (1.2, 0.0, 2.0), 160, 96, flags=vx.FLAG_FULL_QUALITY)
+    imgs, sts = [], []
+    for f in (f22, f0):
+        with _scene(vx, f, noise, dims) as sc:
+            img, st = sc.render(fr, stats=True)
+            assert np.array_equal(sc.read_field()[..., :3], f[..., :3])     # B read back as uploaded
+        imgs.append(img)
+        sts.append(st.as_dict() | {"kernel_ms": 0})
+    assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
+    assert sts[0] == sts[1] and sts[0]["glass_px"] > 100
+    ref, _ = oracle.Oracle(f22, noise).render(fr.params, 160, 96)
+    _compare(imgs[0], ref)
+
+
+def test_hand_edited_map_with_large_radii_uses_the_checked_march(noise):
+    """A map.bin whose R/G values exceed Z (not produced by sdf.cpp) must not
+    take the padded int8 march (its border assumes steps <= Z + 1 cells):
+    vx_scene_create falls back to the bounds-checked march, equal to the oracle."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (96, 48, 16)
+    field = vx.field_build(scenes.small_proc(21, dims=dims, n_boxes=14, n_glass=4))
+    air = field[..., 0] > 0
+    field[..., 0][air] = np.minimum(255, field[..., 0][air].astype(int) * 9).astype(np.uint8)   # R up to 144+
+    field[5, 10, 10, 0] = 200
+    fr = vx.make_frame((48.0, 24.0, 18.0), (1.1, 0.0, 0.6), 128, 80)
+    with _scene(vx, field, noise, dims) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise).render(fr.params, 128, 80)
+    _compare(img, ref)
+    assert st.shadow_fetches == ost.shadow_fetches

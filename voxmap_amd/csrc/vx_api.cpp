@@ -45,6 +45,7 @@ struct vx_scene {
     int8_t *d_sunp = nullptr;     // R, G channels, int8, -1 border (Z <= 126)
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
+    uint8_t *d_bcol = nullptr;    // map.bin's B channel as uploaded (vx_scene_read_field)
     uint32_t *d_noise = nullptr;
     unsigned long long *d_stats = nullptr;
     int *d_tiles = nullptr;
@@ -130,11 +131,17 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
                         field);
         if (rc) return rc;
     }
-    {   // palette index 0xFF is the traversal's border sentinel (vx_kernels.hip primary())
-        const unsigned char *col = from_grid ? static_cast<const unsigned char *>(d->map_bytes) : field.data() + 2;
-        const size_t stride = from_grid ? 1 : 4, n = (size_t)X * Y * Z;
-        for (size_t i = 0; i < n; i++)
-            if (col[i * stride] == 0xFF) return set_error(VX_EINVAL, "map: palette index 255 is reserved");
+    // the padded int8 sun march (march_pad) needs every R/G value <= Z: a step
+    // then moves at most Z + 1 cells per axis and lands in the -1 border of
+    // Z + 2 cells, and no value reads as a negative int8.  sdf.cpp and the GPU
+    // builder cap R at Z and G at z (sdf.cpp:437); a hand-made map.bin may
+    // not, and then the bounds-checked u8 march runs instead.
+    int max_rg = 0;
+    if (!from_grid) {
+        const size_t n = (size_t)X * Y * Z;
+        unsigned char m = 0;
+        for (size_t i = 0; i < n; i++) m = std::max(m, std::max(field[4 * i], field[4 * i + 1]));
+        max_rg = m;
     }
     if (d->noise_path || d->noise_bytes) {
         rc = load_asset(d->noise_path, d->noise_bytes, d->noise_size, d->noise_format, d->key_jwk_k, noise_bytes,
@@ -153,12 +160,13 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     auto fail = [&](int code) { vx_scene_destroy(s); return code; };
     hipError_t e;
     uint8_t *ga = nullptr, *gb = nullptr;
-    uint32_t *lin = nullptr;   // the linear RGBA upload, A rewritten per octant
+    uint32_t *lin = nullptr;   // the linear RGBA upload, B -> vis colour, A rewritten per octant
     if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
         (e = hipMalloc(&lin, field_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
+        (e = hipMalloc(&s->d_bcol, field_bytes / 4)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
         (!from_grid &&
          (e = hipMemcpyAsync(lin, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) ||
@@ -191,11 +199,13 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMalloc(&s->d_sun, 2 * N)) == hipSuccess && (e = hipMalloc(&s->d_rg, 2 * N)) == hipSuccess &&
         (e = hipMalloc(&psum, sizeof(int) * (size_t)(X + 1) * (Y + 1) * (Z + 1))) == hipSuccess &&
         (e = hipMemsetD32Async((hipDeviceptr_t)s->d_prim, 0xFFFFFFFF, 8 * L.texels, s->stream)) == hipSuccess) {
-        lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
+        // B -> vis colour first: the boxes and prim copies classify by it
+        lrc = launch_field_vis(lin, s->d_bcol, X, Y, Z, s->stream);
+        if (!lrc) lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
         if (!lrc) lrc = launch_field_psum(lin, psum, X, Y, Z, s->stream);
         // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
         // march's loaded value carries the exit test (vx_kernels.hip march_fast); values <= Z <= 126
-        if (!lrc && Z <= 126 && (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2)) < (1u << 24)) {
+        if (!lrc && Z <= 126 && max_rg <= Z && (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2)) < (1u << 24)) {
             s->SB = Z + 2;
             s->SXp = X + 2 * s->SB; s->SYp = Y + 2 * s->SB; s->SZp = Z + 2 * s->SB;
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
@@ -230,6 +240,7 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_sun) (void)hipFree(s->d_sun);
     if (s->d_sunp) (void)hipFree(s->d_sunp);
     if (s->d_rg) (void)hipFree(s->d_rg);
+    if (s->d_bcol) (void)hipFree(s->d_bcol);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
@@ -256,8 +267,9 @@ static int read_copy(vx_scene *s, int octant, void *host_out, size_t cap, bool b
     VX_HIP(hipSetDevice(s->device));
     uint32_t *lin = nullptr;
     VX_HIP(hipMalloc(&lin, n));
-    hipError_t e = (hipError_t)launch_field_unpack(boxes ? nullptr : s->d_rg, s->d_prim + (size_t)octant * s->L.texels,
-                                                   lin, s->X, s->Y, s->Z, s->L.pad, s->stream);
+    hipError_t e = (hipError_t)launch_field_unpack(boxes ? nullptr : s->d_rg, s->d_bcol,
+                                                   s->d_prim + (size_t)octant * s->L.texels, lin, s->X, s->Y, s->Z,
+                                                   s->L.pad, s->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, lin, n, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(lin);
@@ -460,6 +472,14 @@ int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tile
               void *frame_device, void *stream) {
     if (!s || !tile_ids || !tiles_device || !frame_device || ts <= 0 || n_tiles <= 0)
         return set_error(VX_EINVAL, "vx_detile: bad arguments");
+    if (w <= 0 || h <= 0 || w > 32768 || h > 32768) return set_error(VX_EINVAL, "vx_detile: frame size out of range");
+    if (fmt != VX_PIXEL_RGBA32F && fmt != VX_PIXEL_RGBA8) return set_error(VX_EINVAL, "vx_detile: unknown pixel format");
+    if (ts % 16) return set_error(VX_EINVAL, "vx_detile: tile_size must be a positive multiple of 16");
+    {
+        const int tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
+        for (int i = 0; i < n_tiles; i++)
+            if (tile_ids[i] < 0 || tile_ids[i] >= tx * ty) return set_error(VX_EINVAL, "vx_detile: tile id out of range");
+    }
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     int rc = upload_ids(st, tile_ids, n_tiles, &s->d_detile, &s->detile_cap, s->h_detile);

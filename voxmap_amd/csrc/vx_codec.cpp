@@ -77,7 +77,15 @@ static int gunzip(const unsigned char *in, size_t n, std::vector<unsigned char> 
     int rc = Z_OK;
     size_t produced = 0;
     for (;;) {
-        if (produced == out.size()) out.resize(out.size() * 2 + 1);
+        if (produced == out.size()) {
+            // a known size bounds the output: a stream that inflates past it is
+            // rejected without growing further (no unbounded allocation)
+            if (expect && produced > expect) {
+                inflateEnd(&zs);
+                return set_error(VX_ESIZE, "gzip stream inflates past the expected " + std::to_string(expect) + " bytes");
+            }
+            out.resize(expect && produced == expect ? expect + 1 : out.size() * 2 + 1);
+        }
         zs.next_out = out.data() + produced;
         zs.avail_out = (uInt)(out.size() - produced);
         rc = inflate(&zs, Z_NO_FLUSH);

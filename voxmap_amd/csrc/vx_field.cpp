@@ -116,11 +116,12 @@ int field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba, int n_
             });
         for (auto &th : pool) th.join();
     }
-    // map.bin texels: R = up, G = down, B = palette index, A = 0 (sdf.cpp:462-470)
+    // map.bin texels: R = up, G = down, B = remapped palette index, A = 0
+    // (sdf.cpp:462-470); the remap turns air into pal_size (sdf.cpp:229-233)
     for (size_t i = 0; i < N; i++) {
         rgba[4 * i + 0] = f.sdf[2 * i + 0];
         rgba[4 * i + 1] = f.sdf[2 * i + 1];
-        rgba[4 * i + 2] = color[i];
+        rgba[4 * i + 2] = color[i] ? color[i] : (uint8_t)VX_PAL_SIZE;
         rgba[4 * i + 3] = 0;
     }
     return VX_OK;

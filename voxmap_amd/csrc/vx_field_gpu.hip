@@ -119,11 +119,13 @@ __global__ void k_plane(const uint8_t *col, const int32_t *pre, uint8_t *sdf, Gr
     cell(col, pre, sdf, g, x, k / g.Z, k % g.Z);   // (y, z) order of the host sweep; any order is exact
 }
 
-// map.bin texels: R = up, G = down, B = palette index, A = 0 (sdf.cpp:462-470)
+// map.bin texels: R = up, G = down, B = remapped palette index (air ->
+// pal_size, sdf.cpp:229-233), A = 0 (sdf.cpp:462-470)
 __global__ void k_texels(const uint8_t *col, const uint8_t *sdf, uint32_t *rgba, size_t N) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
-    rgba[i] = (uint32_t)sdf[2 * i] | ((uint32_t)sdf[2 * i + 1] << 8) | ((uint32_t)col[i] << 16);
+    const uint32_t b = col[i] ? (uint32_t)col[i] : (uint32_t)VX_PAL_SIZE;
+    rgba[i] = (uint32_t)sdf[2 * i] | ((uint32_t)sdf[2 * i + 1] << 8) | (b << 16);
 }
 
 }  // namespace

@@ -111,9 +111,11 @@ int launch_field_psum(const uint32_t *lin, int *S, int X, int Y, int Z, void *st
 // upload with A = an octant's cube sizes (launch_field_octant) -> that octant's prim copy (boxes)
 int launch_field_box(const uint32_t *lin, const int *S, uint32_t *prim_copy, int X, int Y, int Z, int pad, int cap,
                      int oct, void *stream);
-// RGBA of one octant copy, linear
-int launch_field_unpack(const uint16_t *rg, const uint32_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
-                        void *stream);
+// RGBA of one octant copy, linear (B from bcol = map.bin's B channel)
+int launch_field_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t *prim_copy, uint32_t *out, int X,
+                        int Y, int Z, int pad, void *stream);
+// upload's B -> vis colour in place (1..VX_PAL_SIZE-1 kept, else 0), original B into bcol
+int launch_field_vis(uint32_t *lin, uint8_t *bcol, int X, int Y, int Z, void *stream);
 
 // Launchers (vx_kernels.hip).  Return a hipError_t as int.
 int launch_render(const KernelArgs &a, int pixel_format, void *stream);

@@ -175,11 +175,13 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 
 // Field data in HBM, each array shaped for the loop that
 // reads it, so a cache line holds as many useful cells as possible:
-//   prim  8 copies, one per ray octant, u32 per cell: colour | ex << 8 |
-//         ey << 16 | ez << 24, the extents of the all-air box ahead (vxo_field_box),
-//         inside a border of P = cap sentinel cells (0xFFFFFFFF: colour 0xFF is
-//         no palette index, extents are <= cap - 1 <= 254), so the primary
-//         traversal detects leaving the grid from the value it loads;
+//   prim  8 copies, one per ray octant, u32 per cell: vis colour | ex << 8 |
+//         ey << 16 | ez << 24 (vis colour = map.bin B if it is a meshed palette
+//         index 1..21, else 0 = never a surface; extents of the all-unmeshed box
+//         ahead, vxo_field_box), inside a border of P = cap sentinel cells
+//         (0xFFFFFFFF: colour 0xFF is no vis colour, extents are <= cap - 1 <=
+//         254), so the primary traversal detects leaving the grid from the value
+//         it loads;
 //   sun   map.bin's R ("up") and G ("down") channels, u8 each, linear: the
 //         sun march reads one of them;
 //   rg    R | G << 8, u16, linear: the AO trilinear sample.
@@ -422,8 +424,12 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, i
 }
 
 // ---------------- primary visibility ----------------
-// First in-grid colour change along the view ray = the nearest front face of
-// the greedy mesh of sdf.cpp:281-356 after back-face culling.  Box-exit
+// The nearest front face of the greedy mesh of sdf.cpp:281-356 after back-face
+// culling = the first step along the view ray that ENTERS a meshed cell (vis
+// colour 1..21, vx_scene_create) from a cell of another colour.  Air (map.bin
+// B = pal_size = 22, sdf.cpp:229-233) is never meshed (sdf.cpp:284), so a
+// glass -> air step is no surface: glass blends over the next entry behind
+// it (later glass entries are skipped: one blend layer).  Box-exit
 // stepping (oracle/vxo_render.c vxo_primary): in the ray octant's field copy
 // the extents E of a cell say the box [c, c + E*s] ahead of it is air, so one
 // step goes to the face where the ray leaves that box (E = 0: an exact DDA
@@ -498,8 +504,8 @@ __device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d
     float E0 = cvt_f32_ubyte1(t), E1 = cvt_f32_ubyte2(t), E2 = cvt_f32_ubyte3(t);
     // gmark: the colour whose entry is "the first glass" -- glass until a glass
     // entry is recorded, then 256 (matches nothing).  The sentinel's colour
-    // byte 0xFF is no palette index (vx_scene_create), so leaving the grid is
-    // a colour change and the step has a single test: change && !first glass.
+    // byte 0xFF is no vis colour (those are 0..21), so leaving the grid is an
+    // entry that stops the walk.
     int gmark = kGlass, stop, col;
     float g0h = 0.0f, g1h = 0.0f, g2h = 0.0f, gt = 0.0f, te;
     float tb0, tb1, tb2;
@@ -528,14 +534,15 @@ __device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d
         t = fetch(h0, h1, h2);
         cnt.prim_fetch += t >= kSentinel ? 0u : 1u;
         col = t & 0xff;
-        const bool change = col != prev;
-        const bool gfirst = change && col == gmark;
-        if (gfirst) {                                  // glass: blend over the next surface
+        // a face of the mesh: entering a meshed cell (vis colour != 0) from a
+        // cell of another colour; air is never meshed (sdf.cpp:229-233,284)
+        const bool enter = col != prev && col != 0;
+        if (enter && col == gmark) {                   // first glass: blend over the next surface
             gmark = 256;
             g0h = h0; g1h = h1; g2h = h2; gt = te;
             gax = e0 ? 0 : (e1 ? 1 : 2);
         }
-        stop = (change && !gfirst) ? 1 : 0;
+        stop = (enter && col != kGlass) ? 1 : 0;       // later glass entries: single layer
 #if VX_STOP_VGPR
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
 #endif
@@ -955,7 +962,7 @@ __device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o
         cnt.refl_fetch++;
         const int col = t & 0xff;
         e0 = (int)((t >> 8) & 0xff); e1 = (int)((t >> 16) & 0xff); e2 = (int)(t >> 24);
-        if (col != prev) {
+        if (col != prev && col != 0) {                 // entering a meshed cell (air never is)
             const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
             h.color = col;
             h.id = col == kGlass ? 2 : 0;
@@ -1192,7 +1199,7 @@ __global__ void k_detile(const T *tiles, T *frame, int w, int h, int ts, int til
     const int k = (int)(i / per), r = (int)(i % per);
     const int tid = ids[k];
     const int x = (tid % tiles_x) * ts + r % ts, y = (tid / tiles_x) * ts + r / ts;
-    if (x < w && y < h) frame[(size_t)y * w + x] = tiles[i];
+    if (x >= 0 && y >= 0 && x < w && y < h) frame[(size_t)y * w + x] = tiles[i];
 }
 
 // ---- A channel of octant copy `oct`: size r of the air cube ahead of a cell
@@ -1382,10 +1389,25 @@ __global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z
     sunp[j] = (int8_t)(t & 0xffu);
     sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);
 }
-// One octant copy, linear: RGBA (R, G from rg; B = colour; A = the cube size
-// = min(ex, ey, ez), since the box grows from the largest cube) for
-// vx_scene_read_field_copy, or the raw texels (rg == nullptr) for vx_scene_read_boxes
-__global__ void k_unpack(const uint16_t *rg, const uint32_t *prim, uint32_t *dst, int X, int Y, int Z, int P) {
+// map.bin B -> the traversal's vis colour, in place in the linear upload (B
+// kept in bcol for vx_scene_read_field): the meshed palette indices 1..21
+// (sdf.cpp:284 meshes colours < pal_size = 22; render.vert:21) stay, anything
+// else -- air = pal_size (sdf.cpp:229-233, 466-468), 0, >= 22 -- is 0: never a surface
+__global__ void k_vis(uint32_t *lin, uint8_t *bcol, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const uint32_t t = lin[i];
+    const uint32_t b = (t >> 16) & 0xffu;
+    bcol[i] = (uint8_t)b;
+    const uint32_t v = b - 1u < (uint32_t)(VX_PAL_SIZE - 1) ? b : 0u;
+    lin[i] = (t & 0xff00ffffu) | (v << 16);
+}
+// One octant copy, linear: RGBA (R, G from rg; B = map.bin's B from bcol; A =
+// the cube size = min(ex, ey, ez), since the box grows from the largest cube)
+// for vx_scene_read_field_copy, or the raw texels (rg == nullptr: vis colour,
+// ex, ey, ez) for vx_scene_read_boxes
+__global__ void k_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t *prim, uint32_t *dst, int X, int Y,
+                         int Z, int P) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
@@ -1397,7 +1419,7 @@ __global__ void k_unpack(const uint16_t *rg, const uint32_t *prim, uint32_t *dst
     }
     const uint32_t e0 = (p >> 8) & 0xffu, e1 = (p >> 16) & 0xffu, e2 = p >> 24;
     const uint32_t r = min(e0, min(e1, e2));
-    dst[i] = (uint32_t)rg[i] | ((p & 0xffu) << 16) | (r << 24);
+    dst[i] = (uint32_t)rg[i] | ((uint32_t)bcol[i] << 16) | (r << 24);
 }
 }  // namespace
 
@@ -1443,11 +1465,17 @@ int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int S
     return (int)hipGetLastError();
 }
 
-int launch_field_unpack(const uint16_t *rg, const uint32_t *prim_copy, uint32_t *out, int X, int Y, int Z, int pad,
-                        void *stream) {
+int launch_field_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t *prim_copy, uint32_t *out, int X,
+                        int Y, int Z, int pad, void *stream) {
     const size_t N = (size_t)X * Y * Z;
-    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, prim_copy,
-                       out, X, Y, Z, pad);
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, bcol,
+                       prim_copy, out, X, Y, Z, pad);
+    return (int)hipGetLastError();
+}
+
+int launch_field_vis(uint32_t *lin, uint8_t *bcol, int X, int Y, int Z, void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    hipLaunchKernelGGL(k_vis, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lin, bcol, N);
     return (int)hipGetLastError();
 }
 

@@ -62,6 +62,17 @@ def s_proc(seed: int = 1, dims=(1024, 256, 32), n_boxes: int = 400, n_glass: int
 _CAMPUS_HEIGHT = np.array([0, 1, 1, 6, 9, 12, 8, 7, 5, 1, 1, 10, 14, 4, 3, 11, 13, 6, 9, 16, 2, 8], np.int32)
 
 
+NOISE_PATH = os.path.join(_DATA, "noise.bin.gz")
+
+
+def real_noise() -> np.ndarray:
+    """(1024, 1024, 4) RGBA8: the reference's plaintext res/noise.bin.gz
+    (noise.cpp:34-41 layout; render.js:138-149 uploads it as u_noise),
+    shipped as data in voxmap_amd/data/."""
+    with gzip.open(NOISE_PATH, "rb") as f:
+        return np.frombuffer(f.read(), np.uint8).reshape(1024, 1024, 4)
+
+
 def campus_footprint() -> np.ndarray:
     """(Y, X) top-colour map rasterised from the reference's plaintext
     res/vertex2d.bin.gz by tools/make_campus_footprint.py."""
