@@ -4,17 +4,20 @@
 A step renders one full frame of the headline workload (BASELINE configs[2],
 C3: 3840x2160 "full quality" = the reference's v1 shading (primary visibility +
 sun march + AO + sky/clouds + glass) + the f-3 extensions reflection and rough
-normals, on the synthetic S-proc 1024x256x32 field, camera K1) from the
-HBM-resident field into an HBM-resident RGBA8 framebuffer.  The v1 shading
-alone (the reference's own shader, flags 0) is timed in the same run and
-reported under config.v1.  --config C5: the 3^3-upscaled 3072x768x96 field
-with 16-sample soft shadows (BASELINE configs[4]).
+normals, on the synthetic S-proc 1024x256x32 field, camera K1, the reference's
+own res/noise.bin.gz) from the HBM-resident field into an HBM-resident RGBA8
+framebuffer.  In the same N = 1 run: the v1 shading alone (config.v1) and
+BASELINE configs[4] C5 (3^3-upscaled 3072x768x96 field, 16-sample soft
+shadows; config.c5).  --config C5 makes C5 the headline.
 
-N > 1 GPUs (one process per GPU, torchrun): weak scaling — the frame grows
-with N (W = 3840*sqrt(N), H = 2160*sqrt(N), so N = 4 is C4's 7680x4320),
-64x64 screen tiles are dealt round-robin to ranks, each rank renders its tiles
-and rank 0 gathers them over RCCL (torch.distributed "nccl") and de-tiles; the
-gather is inside the timed step.
+N > 1 GPUs (one process per GPU, torchrun): the frame is cut into 64-row
+full-width bands dealt round-robin; each rank renders its bands in place and
+rank 0 gathers them into its frame over RCCL (vx_mgpu_render: native C++,
+ncclSend/ncclRecv in one group; --gather torch runs the same protocol through
+torch.distributed).  The gather is inside the timed step.  --config C3 (the
+driver's default): weak scaling, the frame grows with N (3840*sqrt(N) x
+2160*sqrt(N)); --config C4: BASELINE configs[3], 7680x4320 for every N
+(strong scaling).
 
 Prints ONE JSON line on rank 0.
 """
@@ -31,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-TILE = 64
+BAND = 64               # rows per band of the multi-GPU deal
 
 
 def parse():
@@ -46,213 +49,270 @@ def parse():
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed frames rendered before the warmup so the GPU clock leaves its idle state "
                          "(a ~5 ms burst runs ~12%% slower than steady state: profiles/r01_clock_settle.txt)")
-    ap.add_argument("--config", default="C3")
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--camera", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 measurement of an N = 1 C3 run")
     ap.add_argument("--quality", choices=["full", "v1"], default="full",
                     help="full = v1 + REFLECT + ROUGH (BASELINE 'full quality'); v1 = the reference shader only")
     ap.add_argument("--flags", type=int, default=None, help="VX_FLAG_* bits overriding --quality (diagnostics)")
     ap.add_argument("--samples", type=int, default=None, help="soft-shadow samples (default: 16 for C5, else 1)")
     ap.add_argument("--sun-radius", type=float, default=0.03)
-    ap.add_argument("--traffic-json", default=None,
-                    help="per-launch HBM bytes measured by rocprofv3 PMC (tools/pmc_traffic.py)")
+    ap.add_argument("--gather", choices=["native", "torch"], default="native",
+                    help="N > 1: native = vx_mgpu_render (RCCL from C++); torch = the same bands over "
+                         "torch.distributed 'nccl'")
     return ap.parse_args()
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+def frame_size(cfg_name, cfg, world):
+    """(W, H, scaling) of the run: C4 fixed (strong), else grown by sqrt(N) (weak)."""
+    if cfg_name == "C4" or world == 1:
+        return cfg["w"], cfg["h"], ("strong" if cfg_name == "C4" and world > 1 else "weak")
+    s = math.sqrt(world)
+    return int(round(cfg["w"] * s / 32)) * 32, int(round(cfg["h"] * s / 8)) * 8, "weak"
 
-    import voxmap_amd as vx
-    from voxmap_amd import presets
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if args.gpus > 1 and world == 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-        world = max(world, 1)
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    cfg = presets.CONFIGS[args.config]
-    cam = args.camera or cfg["camera"]
-    scale = math.sqrt(world)
-    W = int(round(cfg["w"] * scale / 16)) * 16
-    H = int(round(cfg["h"] * scale / 16)) * 16
-    up = 3.0 if cfg["scene"] == "s_up3" else 1.0
-
-    grid = presets.scene_grid(cfg["scene"])
-    Z, Y, X = grid.shape
-    noise = vx.noise_synth(0)
-    t_scene = time.perf_counter()
-    # palette grid in, distance field + octant copies built on the device (f-1)
-    scene = vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
-                     noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=local)
-    t_scene = time.perf_counter() - t_scene
-    flags = args.flags if args.flags is not None else (vx.FLAG_FULL_QUALITY if args.quality == "full" else 0)
-    samples = args.samples if args.samples is not None else cfg.get("samples", 1)
-    frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
-                                 sun_radius=args.sun_radius if samples > 1 else 0.0)
-    # K frames in flight: frame i renders on stream i % K into framebuffer
-    # i % K (a swap chain); real streams, so torch events and kernels share them
-    K = max(1, args.inflight)
-    streams = [torch.cuda.Stream() for _ in range(K)]
-    torch.cuda.set_stream(streams[0])
-    stream = streams[0].cuda_stream
-
-    tiles_x, tiles_y = -(-W // TILE), -(-H // TILE)
-    n_tiles = tiles_x * tiles_y
-    if world == 1:
-        outs = [torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") for _ in range(K)]
-        out = outs[0]
-
-        def make_step(j):
-            o, sj = outs[j], streams[j].cuda_stream
-            return lambda: scene.render_device(frame, o.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)
-
-        st = scene.render_device(frame, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
-        stats = st.as_dict()
-    else:
-        from voxmap_amd.dist import ShardedFrame, TileLayout
-        layout = TileLayout(W, H, TILE)
-        shards = []
-        for j in range(K):
-            sj = streams[j].cuda_stream
-            shards.append(ShardedFrame(
-                dist, layout, 4, torch.uint8, "cuda",
-                render_tiles=lambda ids, buf, sj=sj: scene.render_tiles(frame, TILE, ids, buf.data_ptr(),
-                                                                        pixel_format=vx.PIXEL_RGBA8, stream=sj),
-                detile=lambda ids, cat, fr, sj=sj: scene.detile(W, H, TILE, ids, cat.data_ptr(), fr.data_ptr(),
-                                                                pixel_format=vx.PIXEL_RGBA8, stream=sj)))
-
-        def make_step(j):
-            sh, strm = shards[j], streams[j]
-
-            def f():
-                with torch.cuda.stream(strm):      # the gather and de-tile follow this frame's stream
-                    sh.step()
-            return f
-
-        sharded = shards[0]
-        st = scene.render_tiles(frame, TILE, layout.rank_tiles(world, rank), sharded.buf.data_ptr(),
-                                pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
-        keys = [k for k in st.as_dict().keys() if k != "kernel_ms"]
-        vec = torch.tensor([float(st.as_dict()[k]) for k in keys], dtype=torch.float64, device="cuda")
-        dist.all_reduce(vec)
-        stats = {k: float(v) for k, v in zip(keys, vec.tolist())}
-        stats["kernel_ms"] = float(st.kernel_ms)
-    step_fns = [make_step(j) for j in range(K)]
-    n_done = [0]
-
-    def step():
-        step_fns[n_done[0] % K]()
-        n_done[0] += 1
-
-    # clock settle: every rank renders the same number of untimed frames (the
-    # sharded step holds a collective), sized from a short probe to ~settle_ms
-    settle_steps = 0
-    if args.settle_ms > 0:
+def timed(torch, step, steps, warmup, settle_ms, dist=None):
+    """Settle the clock, warm up, then time `steps` frames bracketed by a barrier
+    and a device synchronise on both sides (max over ranks taken by the caller)."""
+    settle = 0
+    if settle_ms > 0:
         torch.cuda.synchronize()
         tp = time.perf_counter()
         for _ in range(3):
             step()
         torch.cuda.synchronize()
         probe_ms = 1000.0 * (time.perf_counter() - tp) / 3
-        n = torch.tensor([math.ceil(args.settle_ms / max(probe_ms, 1e-3))], dtype=torch.int64,
-                         device="cuda" if world > 1 else "cpu")
-        if world > 1:
-            dist.all_reduce(n, op=dist.ReduceOp.MAX)
-        settle_steps = int(min(int(n.item()), 20000)) + 3
-        for _ in range(settle_steps - 3):
+        n = torch.tensor([math.ceil(settle_ms / max(probe_ms, 1e-3))], dtype=torch.int64)
+        if dist is not None:
+            if dist.get_backend() == "nccl":
+                n = n.cuda()
+            dist.all_reduce(n, op=dist.ReduceOp.MAX)     # equal frame counts: the step is collective
+        settle = int(min(int(n.item()), 20000)) + 3
+        for _ in range(settle - 3):
             step()
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    ev_ms = None
-    if world == 1:
-        # per-launch kernel time for the roofline: the same frames on ONE stream,
-        # HIP events on that stream (no overlap; agrees with rocprofv3's average)
-        one = make_step(0)
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        ev0.record()
-        for _ in range(args.steps):
-            one()
-        ev1.record()
-        torch.cuda.synchronize()
-        ev_ms = ev0.elapsed_time(ev1) / args.steps
-    t_local = wall
-    if world > 1:
-        tt = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_local = float(tt.item())
-    ms_per_step = 1000.0 * t_local / args.steps
+    return time.perf_counter() - t0, settle
 
-    v1 = None
+
+def event_ms(torch, one, steps):
+    """Average per-frame kernel time of `one` on the CURRENT stream (the one it
+    launches on), HIP events on that stream, no overlap between frames."""
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev0.record()
+    for _ in range(steps):
+        one()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / steps
+
+
+def pmc_entry(name, config, cam, flags, samples):
+    """A committed rocprofv3 PMC summary (tools/prof_summary.py) for this workload, if any."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        tj = json.load(open(path))
+    except Exception:
+        return None
+    if (tj.get("config") == config and tj.get("camera") == cam and tj.get("flags", 0) == flags
+            and tj.get("samples", 1) == samples):
+        return tj
+    return None
+
+
+def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms):
+    """N = 1: K frames in flight over K streams/framebuffers; timings + stats."""
+    streams = [torch.cuda.Stream() for _ in range(K)]
+    torch.cuda.set_stream(streams[0])
+    outs = [torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") for _ in range(K)]
+    fns = [(lambda o=outs[j], sj=streams[j].cuda_stream:
+            scene.render_device(frame, o.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
+    st = scene.render_device(frame, outs[0].data_ptr(), pixel_format=vx.PIXEL_RGBA8,
+                             stream=streams[0].cuda_stream, stats=True)
+    n = [0]
+
+    def step():
+        fns[n[0] % K]()
+        n[0] += 1
+    wall, settle = timed(torch, step, steps, warmup, settle_ms)
+    ev = event_ms(torch, fns[0], steps)
+    return {"wall_s": wall, "settle": settle, "ev_ms": ev, "stats": st.as_dict()}
+
+
+def roofline_of(alg_bytes, ms):
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    return achieved, achieved / HBM_PEAK_GBPS
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import voxmap_amd as vx
+    from voxmap_amd import presets, scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world == 1:
+        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    world = max(world, 1)
+    torch.cuda.set_device(local)
+    if world > 1:
+        # native gather: RCCL lives in libvoxmap_hip.so; torch.distributed (gloo) only
+        # shares the RCCL unique id, holds the barriers and takes the max time
+        if args.gather == "torch":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+
+    cfg = presets.CONFIGS[args.config]
+    cam = args.camera or cfg["camera"]
+    W, H, scaling = frame_size(args.config, cfg, world)
+    up = 3.0 if cfg["scene"] == "s_up3" else 1.0
+
+    grid = presets.scene_grid(cfg["scene"])
+    Z, Y, X = grid.shape
+    noise = scenes.real_noise()            # the reference's res/noise.bin.gz (u_noise, render.js:138)
+    t_scene = time.perf_counter()
+    # palette grid in, distance field + octant copies built on the device (f-1);
+    # the noise texture through the product's .gz loader
+    scene = vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_path=scenes.NOISE_PATH,
+                     dims=(X, Y, Z), device=local)
+    t_scene = time.perf_counter() - t_scene
+    del grid
+    flags = args.flags if args.flags is not None else (vx.FLAG_FULL_QUALITY if args.quality == "full" else 0)
+    samples = args.samples if args.samples is not None else cfg.get("samples", 1)
+    frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
+                                 sun_radius=args.sun_radius if samples > 1 else 0.0)
+    K = max(1, args.inflight)
+
+    gather_desc = mg = None
+    if world == 1:
+        r = single_gpu(torch, vx, scene, frame, W, H, K, args.steps, args.warmup, args.settle_ms)
+        stats, wall, settle_steps, ev_ms = r["stats"], r["wall_s"], r["settle"], r["ev_ms"]
+    else:
+        streams = [torch.cuda.Stream() for _ in range(K)]
+        torch.cuda.set_stream(streams[0])
+        frames = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(K)]
+        if args.gather == "native":
+            uid = [vx.mgpu_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            mg = vx.MultiGPU(scene, uid[0], world, rank)
+            fns = [(lambda fb=frames[j], sj=streams[j].cuda_stream:
+                    mg.render(frame, BAND, fb.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
+            st = mg.render(frame, BAND, frames[0].data_ptr(), pixel_format=vx.PIXEL_RGBA8,
+                           stream=streams[0].cuda_stream, stats=True)
+            gather_desc = "vx_mgpu_render: one RCCL ncclSend/ncclRecv group into rank 0's frame rows (native C++)"
+        else:
+            from voxmap_amd.dist import BandGather
+            gs = []
+            for j in range(K):
+                sj = streams[j].cuda_stream
+                g = BandGather(dist, W, H, BAND, 4, torch.uint8, "cuda",
+                               lambda ids, fr, sj=sj: scene.render_bands(frame, BAND, ids, fr.data_ptr(),
+                                                                         inplace=True, stream=sj))
+                g.frame = frames[j]
+                gs.append(g)
+
+            def mk(j):
+                def f():
+                    with torch.cuda.stream(streams[j]):
+                        gs[j].step()
+                return f
+            fns = [mk(j) for j in range(K)]
+            st = scene.render_bands(frame, BAND, gs[0].mine, frames[0].data_ptr(), inplace=True,
+                                    stream=streams[0].cuda_stream, stats=True)
+            gather_desc = "torch.distributed batch_isend_irecv (RCCL) into rank 0's frame rows"
+        keys = [k for k in st.as_dict().keys() if k != "kernel_ms"]
+        vec = torch.tensor([float(st.as_dict()[k]) for k in keys], dtype=torch.float64)
+        if args.gather == "torch":
+            vec = vec.cuda()
+        dist.all_reduce(vec)
+        stats = {k: float(v) for k, v in zip(keys, vec.cpu().tolist())}
+        stats["kernel_ms"] = float(st.kernel_ms)
+        n = [0]
+
+        def step():
+            fns[n[0] % K]()
+            n[0] += 1
+        wall, settle_steps = timed(torch, step, args.steps, args.warmup, args.settle_ms, dist)
+        ev_ms = None
+        tt = torch.tensor([wall], dtype=torch.float64)
+        if args.gather == "torch":
+            tt = tt.cuda()
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+    ms_per_step = 1000.0 * wall / args.steps
+
+    v1 = c5 = None
     if world == 1 and flags != 0 and args.flags is None and samples <= 1:
         # the reference's own shader (v1, flags 0) on the same frame: the same
         # K-in-flight wall timing, and one stream with events for its roofline
         fr1 = presets.camera_frame(cam, W, H, scale=up)
-        st1 = scene.render_device(fr1, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=stream, stats=True)
-        v1fns = [(lambda o=outs[j], sj=streams[j].cuda_stream:
-                  scene.render_device(fr1, o.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
-        for i in range(args.warmup):
-            v1fns[i % K]()
-        torch.cuda.synchronize()
-        tw = time.perf_counter()
-        for i in range(args.steps):
-            v1fns[i % K]()
-        torch.cuda.synchronize()
-        ms1w = 1000.0 * (time.perf_counter() - tw) / args.steps
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.steps):
-            v1fns[0]()
-        e1.record()
-        torch.cuda.synchronize()
-        ms1 = e0.elapsed_time(e1) / args.steps
-        r1 = st1.pixels + st1.shadow_rays
+        a = single_gpu(torch, vx, scene, fr1, W, H, K, args.steps, args.warmup, 0.0)
+        s1 = a["stats"]
+        r1 = s1["pixels"] + s1["shadow_rays"]
+        ms1w = 1000.0 * a["wall_s"] / args.steps
         v1 = {"ms_per_frame": round(ms1w, 4), "mrays_per_s": round(r1 / ms1w / 1e3, 3), "rays_per_frame": int(r1),
-              "single_stream_ms_per_frame": round(ms1, 4), "alg_bytes": int(st1.alg_bytes),
-              "roofline_frac": round(st1.alg_bytes / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+              "single_stream_ms_per_frame": round(a["ev_ms"], 4), "alg_bytes": int(s1["alg_bytes"]),
+              "roofline_frac": round(roofline_of(s1["alg_bytes"], a["ev_ms"])[1], 4)}
+    if world == 1 and args.config == "C3" and not args.no_c5 and args.flags is None and args.samples is None:
+        # BASELINE configs[4] in the same run (VERDICT r01: C5 next to C3)
+        c5cfg = presets.CONFIGS["C5"]
+        g5 = presets.scene_grid(c5cfg["scene"])
+        Z5, Y5, X5 = g5.shape
+        t5 = time.perf_counter()
+        sc5 = vx.Scene(map_bytes=g5.tobytes(), map_format=vx.FORMAT_GRID, noise_path=scenes.NOISE_PATH,
+                       dims=(X5, Y5, Z5), device=local)
+        t5 = time.perf_counter() - t5
+        del g5
+        f5 = presets.camera_frame(c5cfg["camera"], c5cfg["w"], c5cfg["h"], scale=3.0, flags=flags,
+                                  shadow_samples=c5cfg["samples"], sun_radius=args.sun_radius)
+        n5 = max(10, args.steps // 5)
+        b = single_gpu(torch, vx, sc5, f5, c5cfg["w"], c5cfg["h"], K, n5, 3, 100.0)
+        s5 = b["stats"]
+        rays5 = s5["pixels"] + s5["shadow_rays"] + s5["reflect_rays"]
+        ms5 = 1000.0 * b["wall_s"] / n5
+        ach5, frac5 = roofline_of(s5["alg_bytes"], b["ev_ms"])
+        t5j = pmc_entry("traffic_r02_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
+        c5 = {"workload": f"C5: {c5cfg['w']}x{c5cfg['h']}, field {X5}x{Y5}x{Z5} (S-proc 3x nearest upsample), "
+                          f"full quality + {c5cfg['samples']}-sample soft shadows (sun radius {args.sun_radius})",
+              "ms_per_frame": round(ms5, 4), "mrays_per_s": round(rays5 / ms5 / 1e3, 3), "fps": round(1000 / ms5, 2),
+              "rays_per_frame": int(rays5), "single_stream_ms_per_frame": round(b["ev_ms"], 4),
+              "alg_bytes": int(s5["alg_bytes"]), "roofline_achieved_gbps": round(ach5, 2),
+              "roofline_frac": round(frac5, 4), "traffic": t5j.get("hbm_bytes_per_launch") if t5j else None,
+              "scene_build_s": round(t5, 3), "frames": n5}
+        sc5.close()
 
     rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
-    value = rays * args.steps / t_local / 1e6                 # whole-job Mrays/s
+    value = rays * args.steps / wall / 1e6                                   # whole-job Mrays/s
     result = None
     if rank == 0:
         per_launch_bytes = float(stats["alg_bytes"]) / world if world > 1 else float(stats["alg_bytes"])
         kernel_ms = ev_ms if world == 1 else stats["kernel_ms"]
-        achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        tj_path = args.traffic_json or os.path.join(
-            ROOT, "profiles", "traffic_r01.json" if args.config != "C5" else "traffic_r01_c5.json")
-        if world == 1 and os.path.exists(tj_path):
-            try:
-                tj = json.load(open(tj_path))
-                if (tj.get("config") == args.config and tj.get("camera") == cam and tj.get("flags", 0) == flags
-                        and tj.get("samples", 1) == samples):
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        achieved, frac = roofline_of(per_launch_bytes, kernel_ms)
+        tag = "r02" if args.config != "C5" else "r02_c5"
+        traffic = pmc_entry(f"traffic_{tag}.json", args.config, cam, flags, samples) if world == 1 else None
+        valu = pmc_entry(f"valu_{tag}.json", args.config, cam, flags, samples) if world == 1 else None
         result = {
             "metric": f"Mrays/s at {cfg['w']}x{cfg['h']} {'full quality' if flags else 'v1 shading'} "
                       f"({args.config}); fps; % HBM roofline",
@@ -263,11 +323,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": f"synthetic {cfg['scene']} field (seed 1) in map.bin layout; synthetic noise texture (real "
-                    "map.blob is AES-encrypted, key not in repo)",
+            "data": f"synthetic {cfg['scene']} field (seed 1) in map.bin layout (the real map.blob is "
+                    "AES-encrypted, key not in the repo); the reference's own res/noise.bin.gz noise texture",
             "config": {
                 "workload": f"{args.config}: {W}x{H} frame, " + (
                     "full quality = v1 shading (primary visibility + sun march + trilinear AO + sky/clouds + glass) "
@@ -278,30 +338,43 @@ def main():
                 "flags": flags, "shadow_samples": samples, "scene_build_s": round(t_scene, 3),
                 "clock_settle": {"ms": args.settle_ms, "untimed_frames": settle_steps},
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
-                "tiles": {"size": TILE, "count": n_tiles, "assignment": "round-robin"} if world > 1 else None,
+                "shards": ({"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
+                            "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc}
+                           if world > 1 else None),
                 "fps": round(1000.0 / ms_per_step, 2),
                 "inflight": {"frames": K, "streams": K, "framebuffers": K,
                              "single_stream_ms_per_frame": round(ev_ms, 4) if ev_ms is not None else None},
                 "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
                 "shadow_rays": int(stats["shadow_rays"]), "reflect_rays": int(stats["reflect_rays"]),
-                "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / t_local / 1e6, 3),
+                "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / wall / 1e6, 3),
                 "v1": v1,
+                "c5": c5,
             },
             "roofline": {
-                "bound": "hbm",
+                # achieved/peak/frac: the contract's unit, algorithmic bytes
+                # over the HBM peak.  "bound" is the resource that measurably binds the
+                # kernel: VALU issue (valu block: rocprofv3 PMC kept under profiles/), the
+                # field being cache-resident (traffic = fabric bytes << algorithmic)
+                "bound": "valu" if valu else "hbm",
                 "kernel": "k_render (fused primary visibility + shading + sun march" +
                           (" + reflection walk" if flags & vx.FLAG_REFLECT else "") + ")",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
+                "frac": round(frac, 4),
+                "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
                 "alg_bytes_per_launch": int(per_launch_bytes),
                 "avg_launch_ms": round(kernel_ms, 4),
+                "fabric_gbps": (round(traffic["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 1)
+                                if traffic else None),
+                "valu": ({k: valu[k] for k in ("valu_busy", "valu_lane_util", "valu_insts_per_wave", "clock_ghz",
+                                               "source") if k in valu} if valu else None),
             },
         }
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(scene, noise, frame, W, H, args.cpu_seconds)
+    if mg is not None:
+        mg.close()
     scene.close()
     if world > 1:
         dist.barrier()
@@ -310,18 +383,31 @@ def main():
         print(json.dumps(result), flush=True)
 
 
+def host_cores():
+    """(threads used, cores this process may run on, the node's hardware_concurrency).
+    The GPU box allots a 1-GPU job 16 host cores (OMP_NUM_THREADS=16 there;
+    os.cpu_count() shows the whole node): the baseline uses the allotment."""
+    node = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:  # pragma: no cover
+        aff = node
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (max(1, min(omp, aff)) if omp > 0 else aff), aff, node
+
+
 def cpu_baseline(scene, noise, frame, W, H, target_s):
     """The scalar oracle (oracle/, -O2 -fno-fast-math -ffp-contract=off, OpenMP
     over rows) on a bounded sample of the same frame: whole frames repeated
     until ~target_s when a frame is cheap (median rate reported), else a
-    deterministic 1-in-k row subset sized to ~target_s."""
+    deterministic 1-in-k row subset sized to ~target_s; then the same on ONE
+    core (a 1-in-k row subset of ~target_s/3)."""
     import numpy as np
 
     import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    dev_field = scene.read_field()            # same bytes (A channel included) the GPU marched
-    o = oracle.Oracle(dev_field, noise)
+    threads, aff, node = host_cores()
+    field = scene.read_field()                # the map.bin bytes the GPU was given (R, G, B)
+    o = oracle.Oracle(field, noise)
     out = np.empty((H, W, 4), np.float32)
     k = 64
     t0 = time.perf_counter()
@@ -344,12 +430,28 @@ def cpu_baseline(scene, noise, frame, W, H, target_s):
         dt = time.perf_counter() - t0
         rates.append((st.pixels + st.shadow_rays + st.reflect_rays) / dt / 1e6)
         desc = f"rows {k // 2}::{k} of the same {W}x{H} frame ({st.pixels} pixels) in {dt:.2f} s"
+    # single core: a 1-in-k row subset of ~target_s/3
+    k1 = 16
+    t0 = time.perf_counter()
+    _, st1 = o.render(frame.params, W, H, row0=k1 // 2, row_step=k1, threads=1, out=out)
+    dt1 = time.perf_counter() - t0
+    k1 = max(1, int(math.ceil(k1 * dt1 / max(target_s / 3, 1e-3))))
+    t0 = time.perf_counter()
+    _, st1 = o.render(frame.params, W, H, row0=k1 // 2, row_step=k1, threads=1, out=out)
+    dt1 = time.perf_counter() - t0
+    single = (st1.pixels + st1.shadow_rays + st1.reflect_rays) / dt1 / 1e6
     return {
         "value": round(float(np.median(rates)), 4),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
         "sample": desc,
+        "single_core": {"value": round(single, 4), "unit": "Mrays/s", "cores": 1,
+                        "sample": f"rows {k1 // 2}::{k1} of the same {W}x{H} frame ({st1.pixels} pixels) "
+                                  f"in {dt1:.2f} s"},
+        "host": {"threads_used": threads, "affinity_cores": aff, "hardware_concurrency": node,
+                 "note": "the GPU box allots 16 host cores to a 1-GPU job (OMP_NUM_THREADS=16); "
+                         "the oracle scales ~linearly over rows (independent pixels)"},
     }
 
 

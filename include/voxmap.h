@@ -12,7 +12,9 @@
  * Conventions: return 0 = OK, < 0 = VX_E* code; the message of the last error
  * on the calling thread is vx_last_error().  A scene owns device memory on one
  * GPU; vx_render* calls are stream-ordered and may run concurrently on
- * different scenes.  No global mutable state besides the thread-local error.
+ * different scenes, and on different streams of one scene -- except calls that
+ * ask for stats: those share the scene's counters and events and must be
+ * serialised per scene.  No global mutable state besides the thread-local error.
  */
 #ifndef VOXMAP_H
 #define VOXMAP_H
@@ -23,7 +25,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 3
+#define VX_ABI_VERSION 4
 
 /* error codes */
 #define VX_OK 0
@@ -108,7 +110,8 @@ typedef struct vx_scene_desc {
  * frame is d = fwd + nx*right + ny*up with nx = (2px+1)/w - 1,
  * ny = 1 - (2py+1)/h (fp32, this operation order). */
 typedef struct vx_frame_params {
-    int quality;                /* u_quality: 0 = 2D mode (base colour), 1 = lit */
+    int quality;                /* u_quality: 0 = MODE_2D (render.js:278,287: the vertex2d footprint
+                                   mesh, unlit), 1 = MODE_3D */
     int frame;                  /* u_frame (unused by render.frag, render.h:9) */
     float time;                 /* u_time = t % 1000 seconds (render.js:293) */
     int cam_cell[3];            /* u_cellPos = floor(camera position) */
@@ -154,6 +157,11 @@ int vx_scene_read_field(vx_scene *scene, void *host_out, size_t cap);
 int vx_scene_read_field_copy(vx_scene *scene, int octant, void *host_out, size_t cap);
 int vx_scene_read_boxes(vx_scene *scene, int octant, void *host_out, size_t cap);
 int vx_scene_dims(const vx_scene *scene, int dims[3]);
+/* The 2D mode mesh of the scene (what sdf.cpp:362-401 writes to
+ * out/vertex2d.bin): the greedy quads of each column's top block (z >= 1) as
+ * 16-byte vert2d records (sdf.cpp:154-173), six per quad.  out == NULL:
+ * size query.  Rendering with quality = 0 draws this mesh (render.js:278). */
+int vx_scene_vertex2d(const vx_scene *scene, void *out, size_t cap, size_t *out_size);
 
 /* --- rendering (replaces gl.drawArrays at render.js:297 + the shaders) --- */
 /* Render a full w*h frame.  out is RGBA32F or RGBA8, row-major, top row
@@ -165,10 +173,9 @@ int vx_render(vx_scene *scene, const vx_frame_params *p, int w, int h, int pixel
               void *out, int out_on_device, void *stream, vx_stats *stats);
 
 /* Render only the listed tile_size x tile_size tiles (tile t covers pixels
- * [(t % tiles_x)*ts, ...) with tiles_x = ceil(w/ts)) into a compact,
- * tile-major device buffer: tile k of the list occupies ts*ts pixels at
- * offset k*ts*ts, row-major inside the tile.  Used for screen-space sharding
- * across GPUs. */
+ * [(t % tiles_x)*ts, ...) with tiles_x = ceil(w/ts); ts a multiple of 32)
+ * into a compact, tile-major device buffer: tile k of the list occupies
+ * ts*ts pixels at offset k*ts*ts, row-major inside the tile. */
 int vx_render_tiles(vx_scene *scene, const vx_frame_params *p, int w, int h, int tile_size,
                     const int *tile_ids, int n_tiles, int pixel_format, void *out_device,
                     void *stream, vx_stats *stats);
@@ -176,6 +183,37 @@ int vx_render_tiles(vx_scene *scene, const vx_frame_params *p, int w, int h, int
 /* Scatter a compact tile-major device buffer back into a w*h frame. */
 int vx_detile(vx_scene *scene, int w, int h, int tile_size, const int *tile_ids, int n_tiles,
               int pixel_format, const void *tiles_device, void *frame_device, void *stream);
+
+/* Render the listed full-width bands of a w*h frame: band b covers rows
+ * [b*band_rows, (b+1)*band_rows) clipped to h; band_rows a multiple of 8.
+ * inplace != 0: out is the w*h frame and each band lands at its own rows
+ * (other rows untouched); inplace == 0: compact, band k of the list at
+ * k*band_rows*w pixels (same row pitch w).  The multi-GPU path's unit. */
+int vx_render_bands(vx_scene *scene, const vx_frame_params *p, int w, int h, int band_rows,
+                    const int *band_ids, int n_bands, int pixel_format, void *out_device,
+                    int inplace, void *stream, vx_stats *stats);
+
+/* --- one frame across the GPUs of a node (RCCL over xGMI) -----
+ * Replaces nothing in the reference (one browser GPU); SURVEY §8(e).  One
+ * process (or thread) per GPU, each with its own vx_scene of the same map.
+ * Rank 0 makes a unique id and shares its VX_MGPU_UID_BYTES bytes out of band
+ * (pipe, file, torch.distributed, MPI); every rank then calls vx_mgpu_create
+ * (collective: blocks until all ranks have joined).  vx_mgpu_render
+ * (collective, stream-ordered) deals full-width bands round-robin (band b ->
+ * rank b % nranks, vx_mgpu_bands), renders each rank's bands in place into its
+ * own w*h frame_device and gathers them into rank 0's frame_device with one
+ * RCCL group of ncclSend/ncclRecv: rank 0's frame is the finished image, no
+ * de-tile pass.  stats: this rank's bands only. */
+#define VX_MGPU_UID_BYTES 128
+typedef struct vx_mgpu vx_mgpu;
+int vx_mgpu_unique_id(void *uid_out);
+int vx_mgpu_create(vx_scene *scene, const void *uid, int nranks, int rank, vx_mgpu **out);
+int vx_mgpu_render(vx_mgpu *m, const vx_frame_params *p, int w, int h, int band_rows, int pixel_format,
+                   void *frame_device, void *stream, vx_stats *stats);
+int vx_mgpu_rank(const vx_mgpu *m, int *nranks, int *rank);
+void vx_mgpu_destroy(vx_mgpu *m);
+/* The deal: the band ids of `rank` (ascending) into ids[0..cap); returns their count. */
+int vx_mgpu_bands(int h, int band_rows, int nranks, int rank, int *ids, int cap);
 
 /* --- host helpers (map.js / math.js / sdf.cpp / utils.js) ----------------- */
 /* map.js:373-391 orbit camera + math.js:37-42 projection (with its sqrt(aspect)
@@ -205,6 +243,10 @@ int vx_field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out,
 /* Same output as vx_field_build, computed on GPU `device` (plane-parallel
  * restatement of the same recurrence; host buffers in and out). */
 int vx_field_build_gpu(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba_out, int device);
+
+/* vertex2d.bin (sdf.cpp:362-401) of a map.bin field (host; no GPU): the 2D
+ * mode mesh vx_scene_vertex2d holds, from RGBA8 texels.  out == NULL: size. */
+int vx_vertex2d(const uint8_t *rgba_field, int X, int Y, int Z, void *out, size_t cap, size_t *out_size);
 
 /* Deterministic synthetic noise texture in noise.bin layout (noise.cpp:34-41). */
 int vx_noise_synth(uint32_t seed, int w, int h, uint8_t *rgba_out);

@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(_HERE, "build", "libvxo.so")
 
 class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
-                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8)]
+                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p)]
 
 
 class OStats(C.Structure):
@@ -100,8 +100,9 @@ class Oracle:
             self.oct_e = [np.ascontiguousarray(e, np.uint8) for e in oct_e]
         for e in self.oct_e:
             assert e.shape == (Z, Y, X, 3)
+        self.fp2d = footprint_2d(self.field)
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
-                         (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]))
+                         (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data)
 
     def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
         """RGBA fp32 (h, w, 4); rows not in (row0::row_step) are NaN."""
@@ -135,6 +136,37 @@ class Oracle:
         d = (C.c_float * 3)()
         lib().vxo_pixel_dir(C.addressof(params), w, h, px, py, d)
         return tuple(d)
+
+
+def footprint(field_zyx4: np.ndarray) -> np.ndarray:
+    """(Y, X) uint8: each column's top block with z >= 1 (a block has R == 0,
+    sdf.cpp:430; z2d starts at 0 and only z > z2d replaces it, sdf.cpp:201-204),
+    its meshed colour (1..21), else 0."""
+    f = np.asarray(field_zyx4)
+    Z = f.shape[0]
+    out = np.zeros(f.shape[1:3], np.uint8)
+    done = np.zeros(f.shape[1:3], bool)
+    for z in range(Z - 1, 0, -1):
+        blk = (f[z, :, :, 0] == 0) & ~done
+        b = f[z, :, :, 2]
+        out[blk] = np.where((b[blk] >= 1) & (b[blk] <= 21), b[blk], 0)
+        done |= blk
+    return out
+
+
+def footprint_2d(field_zyx4: np.ndarray) -> np.ndarray:
+    """(Y, X, 2) uint32 for the oracle's 2D mode: colour, quad corner x0 | y0 << 16
+    of the footprint's greedy quads (mesh_ref.mesh2d: sdf.cpp:362-401, pinned
+    byte for byte against the reference's vertex2d.bin)."""
+    from . import mesh_ref
+    c = footprint(field_zyx4)
+    Y, X = c.shape
+    out = np.zeros((Y, X, 2), np.uint32)
+    out[..., 0] = c
+    c2d = np.where(c == 0, 22, c).T.copy()                 # [x][y], air = pal_size as sdf.cpp remaps it
+    for (x, y, w, h, col, _id) in mesh_ref.mesh2d(c2d):
+        out[y:y + h, x:x + w, 1] = x | (y << 16)
+    return np.ascontiguousarray(out)
 
 
 def field_build(color_zyx: np.ndarray) -> np.ndarray:

@@ -37,6 +37,8 @@ typedef struct {
     const uint8_t *noise;     /* RGBA8 noise texture (render.js:138-149) */
     int noise_w, noise_h;
     const uint8_t *oct_e[8];  /* vxo_field_box per ray octant: 3 extents per cell (primary traversal) */
+    const uint32_t *fp2d;     /* 2D mode (quality 0): per column (x fastest) colour, quad corner x0 | y0 << 16
+                                 of the sdf.cpp:362-401 mesh (oracle/__init__.py footprint_2d); may be NULL */
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */

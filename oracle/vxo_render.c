@@ -680,6 +680,69 @@ static void reflect_color(const shade_ctx *c, const vxo_gbuf *gl, const float rd
     out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
 }
 
+/* 2D mode (u_quality = 0): drawScene binds the vertex2d mesh (render.js:278,
+ * 287): the footprint quads of sdf.cpp:362-401 on the plane z = 0, vert2d
+ * normal byte 0 -> v_normal = (1,0,0) (render.vert:16), culled from below
+ * (render.js:88-91; tri2d winds counter-clockwise seen from +z), drawn over
+ * the clear colour 0.9 (render.js:274-275, from the second frame on).
+ * render.frag with u_quality = 0 outputs baseCol (:241-244); glass (id 2):
+ * alpha = 0.8 exp2(dot(rayDir, n)), rgb *= 0.2 atmCol (:246-249).  The march
+ * and AO it also runs never reach the output there (:244). */
+#define CLEAR_2D 0.9f
+static void shade_2d(const shade_ctx *c, const float d[3], float out[4], vxo_stats *st) {
+    const vxo_scene *s = c->s;
+    const vxo_frame *f = c->f;
+    out[0] = out[1] = out[2] = CLEAR_2D;
+    out[3] = 1.0f;
+    const float zr = (float)(0 - f->cam_cell[2]) - f->cam_fract[2];
+    int col = 0, x = 0, y = 0;
+    float hx = 0.0f, hy = 0.0f;
+    if (zr < 0.0f && d[2] < 0.0f && s->fp2d) {
+        const float t = zr / d[2];
+        hx = f->cam_fract[0] + t * d[0];
+        hy = f->cam_fract[1] + t * d[1];
+        x = f->cam_cell[0] + g_f2i(floorf(hx));
+        y = f->cam_cell[1] + g_f2i(floorf(hy));
+        if (x >= 0 && y >= 0 && x < s->X && y < s->Y) {
+            col = (int)s->fp2d[2 * ((size_t)y * s->X + x)];
+            if (st) st->primary_fetches++;
+        }
+    }
+    if (col == 0) {
+        if (st) st->sky_px++;
+        return;
+    }
+    const uint32_t org = s->fp2d[2 * ((size_t)y * s->X + x) + 1];
+    const int x0 = (int)(org & 0xffffu), y0 = (int)(org >> 16);
+    float base[3];
+    palette(col, base);
+    if (col != GLASS_INDEX) {
+        if (st) st->block_px++;
+        out[0] = base[0]; out[1] = base[1]; out[2] = base[2];
+        return;
+    }
+    if (st) st->glass_px++;
+    /* v_cellPos = the quad corner (x0, y0, 0), v_fractPos = hit - corner */
+    const float fx = (float)(f->cam_cell[0] - x0) + hx, fy = (float)(f->cam_cell[1] - y0) + hy;
+    const float v[3] = {(float)(x0 - f->cam_cell[0]) + (fx - f->cam_fract[0]),
+                        (float)(y0 - f->cam_cell[1]) + (fy - f->cam_fract[1]),
+                        (float)(0 - f->cam_cell[2]) + (0.0f - f->cam_fract[2])};   /* :154 */
+    float r[3];
+    normalize3(v, r);
+    const float n[3] = {1.0f, 0.0f, 0.0f};
+    const float k = 2.0f * dot3(n, r);                                              /* :155 reflect() */
+    const float rz = sqrtf(g_max(0.0f, r[2] - k * n[2]));
+    const float scatter = 1.0f - sqrtf(g_max(0.0f, f->sun_dir[2]));                 /* :168 */
+    const float sp0[3] = {0.2f, 0.4f, 0.7f}, sp1[3] = {0.2f, 0.3f, 0.5f};
+    const float sc0[3] = {0.7f, 0.9f, 1.0f}, sc1[3] = {1.0f, 0.3f, 0.2f};
+    const float a = 0.8f * vxo_exp2(dot3(r, n));                                    /* :247 */
+    for (int i = 0; i < 3; i++) {
+        const float atm = g_mix(g_mix(sc0[i], sc1[i], scatter), g_mix(sp0[i], sp1[i], scatter), rz);   /* :169-171 */
+        const float src = base[i] * (0.2f * atm);                                   /* :248 */
+        out[i] = src * a + CLEAR_2D * (1.0f - a);                                   /* render.js:86 blend */
+    }
+}
+
 /* One pixel: primary visibility, shading, glass blend (render.js:84-86
  * SRC_ALPHA / ONE_MINUS_SRC_ALPHA over the surface behind). */
 static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float out[4], vxo_stats *st) {
@@ -687,6 +750,11 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
     const vxo_frame *f = c->f;
     float d[3];
     vxo_pixel_dir(f, w, h, px, py, d);
+    if (f->quality == 0) {           /* MODE_2D: the vertex2d mesh (render.js:278, 287) */
+        if (st) st->pixels++;
+        shade_2d(c, d, out, st);
+        return;
+    }
     vxo_gbuf g[2];
     int fetches = 0, cap_hit = 0;
     int n = vxo_primary(s, f, d, g, &fetches, &cap_hit);

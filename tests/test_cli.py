@@ -61,3 +61,32 @@ def test_cli_frame_equals_python_host(built, tmp_path, source):
     with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, dims=dims, device=0) as sc:
         want, _ = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
     assert np.array_equal(img, want)
+
+
+@pytest.mark.gpu
+def test_cli_ranks_one_frame_equals_python_host(built, tmp_path):
+    """vxrender --ranks 1: the forked rank process, the RCCL id through the pipe,
+    vx_mgpu_create / vx_mgpu_render (this box has one GPU; N ranks need N GPUs)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    import voxmap_amd as vx
+    from voxmap_amd import presets, scenes
+    dims = (128, 64, 24)
+    grid = scenes.small_proc(11, dims=dims, n_boxes=16, n_glass=8)
+    w, h = 320, 200
+    sbj, rot = (64.0, 32.0, 14.0), (1.2, 0.0, 2.0)
+    path = tmp_path / "map.grid"
+    path.write_bytes(grid.tobytes())
+    out = tmp_path / "frame.rgba"
+    r = subprocess.run([CLI, "--map", str(path), "--format", "grid", "--dims", ",".join(map(str, dims)),
+                        "--size", f"{w},{h}", "--orbit", ",".join(map(str, (*sbj, *rot))), "--full", "--frames", "2",
+                        "--ranks", "1", "--out", str(out)], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["ranks"] == 1 and info["rank0_pixels"] == w * h
+    img = np.frombuffer(out.read_bytes(), np.uint8).reshape(h, w, 4)
+    fr = vx.make_frame(sbj, rot, w, h, hour=presets.SUN_HOUR, time=presets.TIME, flags=vx.FLAG_FULL_QUALITY)
+    with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, dims=dims, device=0) as sc:
+        want, _ = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
+    assert np.array_equal(img, want)

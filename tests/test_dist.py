@@ -1,7 +1,9 @@
-"""Screen-space sharding (voxmap_amd/dist.py) across ranks on CPU with gloo:
-tile deal, padding to equal gather sizes, gather to rank 0, de-tile.  The tile
-renderer is a CPU stand-in (the oracle frame cut into tiles) — on GPUs the same
-ShardedFrame drives vx_render_tiles / vx_detile over RCCL (bench.py)."""
+"""Screen-space sharding across ranks on CPU with gloo (voxmap_amd/dist.py, the
+mirror of the native vx_mgpu_* protocol): band deal, in-place band render,
+point-to-point gather into rank 0's frame rows.  The band renderer is a CPU
+stand-in (rows cut from an oracle frame); on GPUs the same protocol runs in
+C++ over RCCL (vx_mgpu_render, tests/test_parity_gpu.py at one rank, bench.py
+at N ranks), and its deal is vx_mgpu_bands (checked against the mirror here)."""
 import os
 import socket
 
@@ -29,34 +31,29 @@ def _frame():
     return img
 
 
-def _worker(rank, world, port, ts, q, inflight=1, rounds=1):
+def _worker(rank, world, port, band_rows, q, inflight=1, rounds=1):
     import torch
     import torch.distributed as dist
 
-    from voxmap_amd.dist import ShardedFrame, TileLayout, detile_host
+    from voxmap_amd.dist import BandGather, band_rows_of
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         base = _frame()
-        layout = TileLayout(100, 70, ts)
+        H, W = base.shape[:2]
 
         def context(img):
-            padded = np.zeros((layout.tiles_y * ts, layout.tiles_x * ts, 4), np.float32)
-            padded[:70, :100] = img
+            def render_bands(ids, frame):
+                for b in ids:
+                    rows = band_rows_of(b, H, band_rows)
+                    frame[rows] = torch.from_numpy(img[rows])
+            g = BandGather(dist, W, H, band_rows, 4, torch.float32, "cpu", render_bands)
+            g.frame.fill_(float("nan"))       # rows rank 0 neither renders nor receives would show
+            return g
 
-            def render_tiles(ids, buf):
-                for k, t in enumerate(ids):
-                    x0, y0 = (t % layout.tiles_x) * ts, (t // layout.tiles_x) * ts
-                    buf[k] = torch.from_numpy(padded[y0:y0 + ts, x0:x0 + ts])
-
-            def detile(ids, cat, frame):
-                frame.copy_(torch.from_numpy(detile_host(cat.numpy(), layout, ids)))
-
-            return ShardedFrame(dist, layout, 4, torch.float32, "cpu", render_tiles, detile)
-
-        # frames in flight (bench.py --inflight): one ShardedFrame per in-flight
-        # frame, each with its own buffers and content, stepped alternately
+        # frames in flight (bench.py --inflight): one BandGather per in-flight
+        # frame, each with its own frame and content, stepped alternately
         imgs = [base + np.float32(j) for j in range(inflight)]
         ctxs = [context(im) for im in imgs]
         ok = True
@@ -71,13 +68,12 @@ def _worker(rank, world, port, ts, q, inflight=1, rounds=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,ts", [(2, 16), (3, 32), (5, 64)])
-def test_sharded_frame_gloo(built, world, ts):
+def _run(world, band_rows, inflight=1, rounds=1):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ts, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, band_rows, q, inflight, rounds)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -86,33 +82,27 @@ def test_sharded_frame_gloo(built, world, ts):
     assert q.get(timeout=5) is True
 
 
-def test_sharded_frames_in_flight_gloo(built):
+@pytest.mark.parametrize("world,band_rows", [(2, 8), (3, 16), (5, 8), (2, 64)])
+def test_band_gather_gloo(built, world, band_rows):
+    """Ragged last band (70 rows), more ranks than some deals, one band per rank."""
+    _run(world, band_rows)
+
+
+def test_band_gather_frames_in_flight_gloo(built):
     """Two frames in flight (bench.py's double buffering for N > 1): two
-    ShardedFrames stepped alternately keep their own tiles and frames."""
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    world = 2
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 16, q, 2, 3)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=180)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert q.get(timeout=5) is True
+    BandGathers stepped alternately keep their own frames."""
+    _run(2, 16, inflight=2, rounds=3)
 
 
-def test_tile_layout_deal_is_a_partition():
-    from voxmap_amd.dist import TileLayout
-    lay = TileLayout(3840, 2160, 64)
-    assert lay.n_tiles == 60 * 34
-    for world in (1, 2, 4, 8, 7):
-        lists = [lay.rank_tiles(world, r) for r in range(world)]
-        flat = sorted(t for l in lists for t in l)
-        assert flat == list(range(lay.n_tiles))
-        padded, concat, per = lay.padded(world)
-        assert all(len(l) == per for l in padded) and len(concat) == per * world
-    tiny = TileLayout(10, 10, 16)
-    padded, concat, per = tiny.padded(4)        # more ranks than tiles
-    assert per == 1 and concat == [0, 0, 0, 0]
+def test_band_deal_is_a_partition_and_matches_native(built):
+    import voxmap_amd as vx
+    from voxmap_amd.dist import bands, n_bands
+    for h, br in ((4320, 64), (2160, 32), (70, 8), (8, 8), (6112, 64)):
+        for world in (1, 2, 4, 7, 8):
+            lists = [bands(h, br, world, r) for r in range(world)]
+            flat = sorted(t for l in lists for t in l)
+            assert flat == list(range(n_bands(h, br)))
+            sizes = [len(l) for l in lists]
+            assert max(sizes) - min(sizes) <= 1                      # balanced to one band
+            for r in range(world):
+                assert vx.mgpu_bands(h, br, world, r) == lists[r]    # the native deal (vx_mgpu_bands)

@@ -95,3 +95,18 @@ def test_fixtures_are_the_reference_assets():
     from voxmap_amd import scenes
     assert open(scenes.NOISE_PATH, "rb").read() == open("/root/reference/res/noise.bin.gz", "rb").read()
     assert open(V2D, "rb").read() == open("/root/reference/res/vertex2d.bin.gz", "rb").read()
+
+
+def test_vertex2d_regenerated_from_the_campus_map(built, v2d):
+    """End to end through the product's host code: S-campus as map.bin (the
+    footprint extruded, air = B 22) -> vx_vertex2d (each column's top block,
+    sdf.cpp:201-204, meshed by the C++ restatement of sdf.cpp:362-401) == the
+    reference's vertex2d.bin byte for byte; the oracle's footprint + mesher too."""
+    import oracle
+    import voxmap_amd as vx
+    from oracle import mesh_ref
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_campus"))
+    assert vx.vertex2d(field) == v2d
+    c = oracle.footprint(field)
+    assert mesh_ref.vertex2d_bytes(mesh_ref.mesh2d(np.where(c == 0, 22, c).T.copy())) == v2d

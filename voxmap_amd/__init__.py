@@ -8,8 +8,9 @@ itself and raises if the library is missing.
 from ._abi import (FLAG_FULL_QUALITY, FLAG_INT_INDEX, FLAG_NO_AO, FLAG_NO_CLOUDS, FLAG_NO_SHADOW, FLAG_PRIMARY_ONLY, FLAG_REFLECT,
                    FLAG_ROUGH, FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB, FORMAT_GRID, PIXEL_RGBA8, PIXEL_RGBA32F,
                    FrameParams, Stats, VoxmapError, lib)
-from .renderer import (Frame, Scene, blob_encrypt, decode, field_build, frame_from_matrix, frame_from_orbit,
-                       hour_from_time_ms, make_frame, noise_synth, field_build_gpu, params_to_dict, sun_from_hour, sun_samples)
+from .renderer import (Frame, MultiGPU, Scene, blob_encrypt, decode, field_build, frame_from_matrix, frame_from_orbit,
+                       hour_from_time_ms, make_frame, mgpu_bands, mgpu_unique_id, noise_synth, field_build_gpu,
+                       params_to_dict, sun_from_hour, sun_samples, vertex2d)
 
 __all__ = [
     "Scene", "Frame", "FrameParams", "Stats", "VoxmapError", "lib", "make_frame", "frame_from_orbit",
@@ -17,4 +18,5 @@ __all__ = [
     "blob_encrypt", "params_to_dict", "PIXEL_RGBA32F", "PIXEL_RGBA8", "FORMAT_AUTO", "FORMAT_BIN",
     "FORMAT_BIN_GZ", "FORMAT_BLOB", "FLAG_NO_SHADOW", "FLAG_NO_AO", "FLAG_NO_CLOUDS", "FLAG_PRIMARY_ONLY",
     "FLAG_REFLECT", "FLAG_ROUGH", "FLAG_FULL_QUALITY", "FLAG_INT_INDEX", "sun_samples", "field_build_gpu", "FORMAT_GRID",
+    "MultiGPU", "mgpu_unique_id", "mgpu_bands", "vertex2d",
 ]

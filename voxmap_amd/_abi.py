@@ -28,7 +28,9 @@ FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
 FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
 FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary index path
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 3
+ABI_VERSION = 4
+PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
+MGPU_UID_BYTES = 128
 
 
 class SceneDesc(C.Structure):
@@ -80,6 +82,7 @@ SIGNATURES = [
     ("vx_scene_read_field_copy", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("vx_scene_read_boxes", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("vx_scene_dims", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    ("vx_scene_vertex2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("vx_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
                             C.c_void_p, C.c_int, C.c_void_p, C.POINTER(Stats)]),
     ("vx_render_tiles", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
@@ -87,6 +90,16 @@ SIGNATURES = [
                                   C.POINTER(Stats)]),
     ("vx_detile", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int,
                             C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("vx_render_bands", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
+                                  C.POINTER(C.c_int), C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                  C.POINTER(Stats)]),
+    ("vx_mgpu_unique_id", C.c_int, [C.c_void_p]),
+    ("vx_mgpu_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    ("vx_mgpu_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_void_p, C.c_void_p, C.POINTER(Stats)]),
+    ("vx_mgpu_rank", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("vx_mgpu_destroy", None, [C.c_void_p]),
+    ("vx_mgpu_bands", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int]),
     ("vx_frame_from_orbit", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
                                       C.POINTER(FrameParams)]),
     ("vx_frame_from_matrix", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(FrameParams)]),
@@ -97,6 +110,8 @@ SIGNATURES = [
     ("vx_blob_encrypt", C.c_int, [C.c_void_p, C.c_size_t, C.c_char_p, C.c_void_p, C.c_size_t,
                                   C.POINTER(C.c_size_t)]),
     ("vx_field_build", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
+    ("vx_vertex2d", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                              C.POINTER(C.c_size_t)]),
     ("vx_noise_synth", C.c_int, [C.c_uint32, C.c_int, C.c_int, C.c_void_p]),
     ("vx_field_build_gpu", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
     ("vx_last_error", C.c_char_p, []),

@@ -14,12 +14,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libvoxmap_hip.so")
-SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_kernels.hip", "vx_field_gpu.hip"]
+SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_mgpu.cpp", "vx_kernels.hip",
+           "vx_field_gpu.hip"]
 ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
 # -fno-slp-vectorize: packed FP32 (v_pk_*) issues at the cost of two scalar ops
 # on gfx950 (profiles/r01_valu_costs.txt), so SLP packing only adds moves.
 FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", f"--offload-arch={ARCH}"]
-LIBS = ["-lz", "-lcrypto", "-lpthread"]
+LIBS = ["-lz", "-lcrypto", "-lpthread", "-lrccl"]
 
 
 def hipcc() -> str:
@@ -58,8 +59,30 @@ def build(force: bool = False, verbose: bool = True, out: str | None = None, def
     if out is None and not defines and not extra_flags and not force and not needs_build():
         return OUT
     tmp = target + ".tmp"
-    cmd = [hipcc(), *FLAGS, *extra_flags, *[f"-D{d}" for d in defines], "-shared", "-o", tmp,
-           *[os.path.join(CSRC, s) for s in SOURCES], *LIBS]
+    # one object per source, compiled in parallel (the kernels file dominates)
+    tag = os.path.basename(target).replace(".", "_")
+    objdir = os.path.join(HERE, "build", tag)
+    os.makedirs(objdir, exist_ok=True)
+    flags = [*FLAGS, *extra_flags, *[f"-D{d}" for d in defines]]
+    jobs, objs = [], []
+    hdrs = [os.path.join(CSRC, "vx_internal.h"), os.path.join(HERE, "..", "include", "voxmap.h"), __file__]
+    for src in SOURCES:
+        obj = os.path.join(objdir, src + ".o")
+        objs.append(obj)
+        # incremental unless forced: an object newer than its source and the headers is kept
+        if not force and os.path.exists(obj) and all(os.path.getmtime(obj) > os.path.getmtime(d)
+                                                     for d in [os.path.join(CSRC, src), *hdrs]):
+            continue
+        cmd = [hipcc(), *flags, "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        jobs.append((cmd, obj))
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), os.cpu_count() or 1, 8))) as ex:
+        for r in list(ex.map(lambda j: subprocess.run(j[0]), jobs)):
+            if r.returncode:
+                raise subprocess.CalledProcessError(r.returncode, r.args)
+    cmd = [hipcc(), *flags, "-shared", "-o", tmp, *objs, *LIBS]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

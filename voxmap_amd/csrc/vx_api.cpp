@@ -46,13 +46,17 @@ struct vx_scene {
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
     uint8_t *d_bcol = nullptr;    // map.bin's B channel as uploaded (vx_scene_read_field)
+    uint32_t *d_fp2d = nullptr;   // 2D mode: per column vis colour + quad corner (KernelArgs::fp2d)
+    std::vector<Quad2d> quads2d;  // 2D mode: the footprint's greedy quads (vx_scene_vertex2d)
     uint32_t *d_noise = nullptr;
     unsigned long long *d_stats = nullptr;
     int *d_tiles = nullptr;
     int tiles_cap = 0;
     int *d_detile = nullptr;
     int detile_cap = 0;
-    std::vector<int> h_tiles, h_detile;   // last lists uploaded to d_tiles / d_detile
+    int *d_bands = nullptr;
+    int bands_cap = 0;
+    std::vector<int> h_tiles, h_detile, h_bands;   // last lists uploaded to d_tiles / d_detile / d_bands
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     FieldLayout L;
@@ -64,6 +68,8 @@ struct vx_scene {
         if (e_ != hipSuccess)                                                                        \
             return set_error(VX_EDEVICE, std::string(#call " failed: ") + hipGetErrorString(e_));     \
     } while (0)
+
+int vx::scene_device(const vx_scene *s) { return s->device; }
 
 static int read_file(const char *path, std::vector<unsigned char> &buf) {
     std::ifstream f(path, std::ios::binary);
@@ -98,9 +104,43 @@ static int load_asset(const char *path, const void *bytes, size_t size, int form
     return VX_OK;
 }
 
+// 2D mode data (DESIGN.md §3 "2D mode"): the footprint of the field (each
+// column's top block with z >= 1, sdf.cpp:201-204) meshed by the greedy 2D
+// mesher of sdf.cpp:362-401 on the host, uploaded as {colour, quad corner}
+// per column.  Returns a hipError_t as int.
+static int build_2d(vx_scene *s, const uint32_t *d_lin) {
+    const size_t n = (size_t)s->X * s->Y;
+    uint8_t *d_c2d = nullptr;
+    hipError_t e = hipMalloc(&d_c2d, n);
+    std::vector<uint8_t> c2d(n);
+    if (e == hipSuccess) e = (hipError_t)launch_footprint(d_lin, d_c2d, s->X, s->Y, s->Z, s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(c2d.data(), d_c2d, n, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (d_c2d) (void)hipFree(d_c2d);
+    if (e != hipSuccess) return (int)e;
+    std::vector<uint32_t> origin(n, 0), fp(2 * n);
+    mesh2d(c2d.data(), s->X, s->Y, s->quads2d, origin.data());
+    for (size_t i = 0; i < n; i++) {
+        fp[2 * i] = c2d[i];
+        fp[2 * i + 1] = origin[i];
+    }
+    e = hipMalloc(&s->d_fp2d, fp.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(s->d_fp2d, fp.data(), fp.size() * 4, hipMemcpyHostToDevice);
+    return (int)e;
+}
+
 extern "C" {
 
 const char *vx_last_error(void) { return g_err.c_str(); }
+
+int vx_scene_vertex2d(const vx_scene *s, void *out, size_t cap, size_t *out_size) {
+    if (!s || !out_size) return set_error(VX_EINVAL, "vx_scene_vertex2d: null argument");
+    *out_size = vertex2d_bytes(s->quads2d, nullptr, 0);
+    if (!out) return VX_OK;
+    if (cap < *out_size) return set_error(VX_EINVAL, "vx_scene_vertex2d: output buffer too small");
+    vertex2d_bytes(s->quads2d, static_cast<uint8_t *>(out), cap);
+    return VX_OK;
+}
 int vx_abi_version(void) { return VX_ABI_VERSION; }
 
 int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
@@ -201,6 +241,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMemsetD32Async((hipDeviceptr_t)s->d_prim, 0xFFFFFFFF, 8 * L.texels, s->stream)) == hipSuccess) {
         // B -> vis colour first: the boxes and prim copies classify by it
         lrc = launch_field_vis(lin, s->d_bcol, X, Y, Z, s->stream);
+        if (!lrc) lrc = build_2d(s, lin);
         if (!lrc) lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
         if (!lrc) lrc = launch_field_psum(lin, psum, X, Y, Z, s->stream);
         // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
@@ -241,10 +282,12 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_sunp) (void)hipFree(s->d_sunp);
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_bcol) (void)hipFree(s->d_bcol);
+    if (s->d_fp2d) (void)hipFree(s->d_fp2d);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     if (s->d_detile) (void)hipFree(s->d_detile);
+    if (s->d_bands) (void)hipFree(s->d_bands);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -334,8 +377,17 @@ static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int 
     st->kernel_ms = ms;
 }
 
-static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts, const int *tile_ids, int n_tiles,
-                     int fmt, void *out_dev, void *stream, vx_stats *stats) {
+// A tiled launch: tiles of tw x th pixels (multiples of the 32 x 8 kernel
+// block), tiles_x per tile row; compact output (tile k at k * th * pitch
+// pixels, rows pitch pixels apart) or in place in the w-wide frame.
+struct TileSpec {
+    int tw = 0, th = 0, pitch = 0, tiles_x = 0, inplace = 0;
+    const int *ids = nullptr;   // device list
+    int n = 0;
+};
+
+static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const TileSpec &ts, int fmt, void *out_dev,
+                     void *stream, vx_stats *stats) {
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     KernelArgs a;
     std::memset(&a, 0, sizeof a);
@@ -348,6 +400,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.sunp_texels = a.SXpYp * (unsigned)s->SZp;
     a.rg = s->d_rg;
     a.noise = s->d_noise;
+    a.fp2d = s->d_fp2d;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;
     a.noise_w = s->noise_w; a.noise_h = s->noise_h;
     a.noise_rw = 1.0f / (float)s->noise_w;   // powers of two: exact
@@ -355,10 +408,13 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, int ts
     a.noise_lw = 0;
     while ((1 << a.noise_lw) < s->noise_w) a.noise_lw++;
     a.w = w; a.h = h;
-    a.tile_size = ts;
-    a.tiles_x = ts ? (w + ts - 1) / ts : 0;
-    a.tile_ids = tile_ids;
-    a.n_tiles = n_tiles;
+    a.tile_w = ts.tw;
+    a.tile_h = ts.th;
+    a.tile_pitch = ts.pitch;
+    a.tiles_x = ts.tiles_x;
+    a.tile_inplace = ts.inplace;
+    a.tile_ids = ts.ids;
+    a.n_tiles = ts.n;
     a.out = out_dev;
     a.p = *p;
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
@@ -413,11 +469,11 @@ int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void
     if (!out) return set_error(VX_EINVAL, "vx_render: null output");
     VX_HIP(hipSetDevice(s->device));
     const size_t bytes = (size_t)w * h * (fmt == VX_PIXEL_RGBA32F ? 16 : 4);
-    if (out_on_device) return do_render(s, p, w, h, 0, nullptr, 0, fmt, out, stream, stats);
+    if (out_on_device) return do_render(s, p, w, h, TileSpec(), fmt, out, stream, stats);
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     void *d_out = nullptr;
     VX_HIP(hipMallocAsync(&d_out, bytes, st));
-    rc = do_render(s, p, w, h, 0, nullptr, 0, fmt, d_out, st, stats);
+    rc = do_render(s, p, w, h, TileSpec(), fmt, d_out, st, stats);
     if (rc == VX_OK) {
         hipError_t e = hipMemcpyAsync(out, d_out, bytes, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -456,7 +512,7 @@ int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts,
                     int fmt, void *out_device, void *stream, vx_stats *stats) {
     int rc = check_params(s, p, w, h, fmt);
     if (rc) return rc;
-    if (ts <= 0 || ts % 16) return set_error(VX_EINVAL, "tile_size must be a positive multiple of 16");
+    if (ts <= 0 || ts % VX_TILE_ALIGN_X) return set_error(VX_EINVAL, "tile_size must be a positive multiple of 32");
     if (!tile_ids || n_tiles <= 0 || !out_device) return set_error(VX_EINVAL, "vx_render_tiles: empty tile list");
     const int tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
     for (int i = 0; i < n_tiles; i++)
@@ -465,7 +521,37 @@ int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts,
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     rc = upload_ids(st, tile_ids, n_tiles, &s->d_tiles, &s->tiles_cap, s->h_tiles);
     if (rc) return rc;
-    return do_render(s, p, w, h, ts, s->d_tiles, n_tiles, fmt, out_device, st, stats);
+    TileSpec t;
+    t.tw = t.th = t.pitch = ts;
+    t.tiles_x = tx;
+    t.ids = s->d_tiles;
+    t.n = n_tiles;
+    return do_render(s, p, w, h, t, fmt, out_device, st, stats);
+}
+
+int vx_render_bands(vx_scene *s, const vx_frame_params *p, int w, int h, int band_rows, const int *band_ids,
+                    int n_bands, int fmt, void *out_device, int inplace, void *stream, vx_stats *stats) {
+    int rc = check_params(s, p, w, h, fmt);
+    if (rc) return rc;
+    if (band_rows <= 0 || band_rows % VX_TILE_ALIGN_Y)
+        return set_error(VX_EINVAL, "band_rows must be a positive multiple of 8");
+    if (!band_ids || n_bands <= 0 || !out_device) return set_error(VX_EINVAL, "vx_render_bands: empty band list");
+    const int nb = (h + band_rows - 1) / band_rows;
+    for (int i = 0; i < n_bands; i++)
+        if (band_ids[i] < 0 || band_ids[i] >= nb) return set_error(VX_EINVAL, "band id out of range");
+    VX_HIP(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    rc = upload_ids(st, band_ids, n_bands, &s->d_bands, &s->bands_cap, s->h_bands);
+    if (rc) return rc;
+    TileSpec t;
+    t.tw = (w + VX_TILE_ALIGN_X - 1) / VX_TILE_ALIGN_X * VX_TILE_ALIGN_X;   // one tile spans the row
+    t.th = band_rows;
+    t.pitch = w;                      // compact bands keep the frame's row pitch
+    t.tiles_x = 1;
+    t.inplace = inplace ? 1 : 0;
+    t.ids = s->d_bands;
+    t.n = n_bands;
+    return do_render(s, p, w, h, t, fmt, out_device, st, stats);
 }
 
 int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tiles, int fmt, const void *tiles_device,
@@ -474,7 +560,7 @@ int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tile
         return set_error(VX_EINVAL, "vx_detile: bad arguments");
     if (w <= 0 || h <= 0 || w > 32768 || h > 32768) return set_error(VX_EINVAL, "vx_detile: frame size out of range");
     if (fmt != VX_PIXEL_RGBA32F && fmt != VX_PIXEL_RGBA8) return set_error(VX_EINVAL, "vx_detile: unknown pixel format");
-    if (ts % 16) return set_error(VX_EINVAL, "vx_detile: tile_size must be a positive multiple of 16");
+    if (ts % VX_TILE_ALIGN_X) return set_error(VX_EINVAL, "vx_detile: tile_size must be a positive multiple of 32");
     {
         const int tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
         for (int i = 0; i < n_tiles; i++)

@@ -5,13 +5,19 @@
 //   updateState camera / sun (map.js:349-402)  -> vx_frame_from_orbit, vx_sun_from_hour
 //   drawScene + gl.drawArrays (render.js:267)  -> vx_render into a device framebuffer
 //   canvas.toDataURL (map.js:185)              -> the RGBA8 frame written as .ppm / .rgba
+//   --ranks N: one frame across N GPUs (devices D..D+N-1): one process per GPU
+//   forked before any HIP call, rank 0's RCCL unique id passed through a pipe,
+//   vx_mgpu_render gathers the bands into rank 0's frame (include/voxmap.h)
 //
 // usage: vxrender --map FILE [--format bin|gz|blob|grid] [--key JWK_K] [--noise FILE]
 //                 [--dims X,Y,Z] [--size W,H] [--camera K0|K1|K2 | --orbit sx,sy,sz,rx,ry,rz]
 //                 [--hour H] [--time T] [--flags N] [--full] [--samples N] [--radius R]
-//                 [--frames N] [--device D] [--out FILE.ppm|FILE.rgba]
+//                 [--frames N] [--device D] [--ranks N] [--out FILE.ppm|FILE.rgba]
 // The key may also come from the VOXMAP_KEY environment variable (never a file in the repository).
 #include <hip/hip_runtime.h>
+
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cmath>
@@ -62,7 +68,7 @@ std::vector<unsigned char> read_all(const std::string &path) {
 
 int main(int argc, char **argv) {
     std::string map, noise, key, out, format = "auto";
-    int dims[3] = {1024, 256, 32}, w = 3840, h = 2160, frames = 1, device = 0, samples = 0;
+    int dims[3] = {1024, 256, 32}, w = 3840, h = 2160, frames = 1, device = 0, samples = 0, ranks = 0;
     double sbj[3] = {381.5, 128.1, 40.0}, rot[3] = {1.1, 0.0, 0.6};   // camera K1 (voxmap_amd/presets.py)
     double hour = 1.0, time = 123.0, radius = 0.03;
     unsigned flags = 0;
@@ -94,17 +100,43 @@ int main(int argc, char **argv) {
         else if (a == "--radius") radius = std::atof(next());
         else if (a == "--frames") frames = std::atoi(next());
         else if (a == "--device") device = std::atoi(next());
+        else if (a == "--ranks") ranks = std::atoi(next());
         else if (a == "--out") out = next();
         else if (a == "--help" || a == "-h") {
             std::printf("usage: vxrender --map FILE [--format bin|gz|blob|grid] [--key K] [--noise FILE] "
                         "[--dims X,Y,Z] [--size W,H] [--camera K0|K1|K2 | --orbit sx,sy,sz,rx,ry,rz] [--hour H] "
                         "[--time T] [--flags N] [--full] [--samples N] [--radius R] [--frames N] [--device D] "
-                        "[--out FILE.ppm|FILE.rgba]\n(ABI version %d)\n", vx_abi_version());
+                        "[--ranks N] [--out FILE.ppm|FILE.rgba]\n(ABI version %d)\n", vx_abi_version());
             return 0;
         } else die("unknown option " + a);
     }
     if (map.empty()) die("--map is required (see --help)");
     if (key.empty() && std::getenv("VOXMAP_KEY")) key = std::getenv("VOXMAP_KEY");
+    if (ranks < 0 || ranks > 64) die("--ranks must be in 0..64");
+
+    // --ranks N: fork the rank processes now, before anything touches the GPU
+    int rank = 0, nranks = 1, uid_pipe[2] = {-1, -1};
+    if (ranks >= 1) {
+        nranks = ranks;
+        if (pipe(uid_pipe) != 0) die("pipe failed");
+        std::vector<pid_t> kids;
+        for (int r = 0; r < nranks; r++) {
+            const pid_t pid = fork();
+            if (pid < 0) die("fork failed");
+            if (pid == 0) { rank = r; kids.clear(); break; }
+            kids.push_back(pid);
+        }
+        if (!kids.empty()) {                         // the parent: wait for every rank
+            close(uid_pipe[0]); close(uid_pipe[1]);
+            int rc = 0;
+            for (pid_t k : kids) {
+                int stw = 0;
+                if (waitpid(k, &stw, 0) < 0 || !WIFEXITED(stw) || WEXITSTATUS(stw) != 0) rc = 2;
+            }
+            return rc;
+        }
+        device += rank;
+    }
 
     const std::vector<unsigned char> bytes = read_all(map);
     vx_scene_desc d = {};
@@ -143,27 +175,52 @@ int main(int argc, char **argv) {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreate(&stream) != hipSuccess ||
         hipMalloc(&d_out, bytes_out) != hipSuccess)
         die("device framebuffer allocation failed");
+    vx_mgpu *mg = nullptr;
+    if (ranks >= 1) {                                // rank 0 makes the RCCL id, the others read it
+        unsigned char uid[VX_MGPU_UID_BYTES];
+        if (rank == 0) {
+            check(vx_mgpu_unique_id(uid), "vx_mgpu_unique_id");
+            for (int r = 1; r < nranks; r++)
+                if (write(uid_pipe[1], uid, sizeof uid) != (ssize_t)sizeof uid) die("pipe write failed");
+        } else {
+            size_t got = 0;
+            while (got < sizeof uid) {
+                const ssize_t n = read(uid_pipe[0], uid + got, sizeof uid - got);
+                if (n <= 0) die("pipe read failed");
+                got += (size_t)n;
+            }
+        }
+        close(uid_pipe[0]); close(uid_pipe[1]);
+        check(vx_mgpu_create(scene, uid, nranks, rank, &mg), "vx_mgpu_create");
+    }
+    auto draw = [&](vx_stats *s) {
+        if (mg) check(vx_mgpu_render(mg, &p, w, h, 64, VX_PIXEL_RGBA8, d_out, stream, s), "vx_mgpu_render");
+        else check(vx_render(scene, &p, w, h, VX_PIXEL_RGBA8, d_out, 1, stream, s), "vx_render");
+    };
     vx_stats st = {};
-    check(vx_render(scene, &p, w, h, VX_PIXEL_RGBA8, d_out, 1, stream, &st), "vx_render");   // counters
+    draw(&st);                                        // counters (this rank's pixels)
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, stream);
-    for (int f = 0; f < frames; f++)
-        check(vx_render(scene, &p, w, h, VX_PIXEL_RGBA8, d_out, 1, stream, nullptr), "vx_render");
+    for (int f = 0; f < frames; f++) draw(nullptr);
     (void)hipEventRecord(e1, stream);
     (void)hipEventSynchronize(e1);
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, e0, e1);
     ms /= (float)frames;
     const double rays = (double)(st.pixels + st.shadow_rays + st.reflect_rays);
-    std::printf("{\"size\": [%d, %d], \"field\": [%d, %d, %d], \"flags\": %u, \"shadow_samples\": %d, "
-                "\"scene_build_s\": %.3f, \"ms_per_frame\": %.4f, \"fps\": %.1f, \"mrays_per_s\": %.1f, "
-                "\"alg_gbps\": %.1f, \"rays_per_frame\": %.0f}\n",
-                w, h, dims[0], dims[1], dims[2], flags, samples, scene_s, ms, 1000.0 / ms, rays / ms / 1e3,
-                (double)st.alg_bytes / ms / 1e6, rays);
+    if (rank == 0)
+        std::printf("{\"size\": [%d, %d], \"field\": [%d, %d, %d], \"flags\": %u, \"shadow_samples\": %d, "
+                    "\"ranks\": %d, \"scene_build_s\": %.3f, \"ms_per_frame\": %.4f, \"fps\": %.1f, "
+                    "\"rank0_pixels\": %llu, \"rank0_mrays_per_s\": %.1f, \"rank0_alg_gbps\": %.1f, "
+                    "\"rank0_rays_per_frame\": %.0f}\n",
+                    w, h, dims[0], dims[1], dims[2], flags, samples, nranks, scene_s, ms, 1000.0 / ms,
+                    (unsigned long long)st.pixels, rays / ms / 1e3, (double)st.alg_bytes / ms / 1e6, rays);
+    std::fflush(stdout);
+    if (mg) vx_mgpu_destroy(mg);
 
-    if (!out.empty()) {
+    if (!out.empty() && rank == 0) {
         std::vector<unsigned char> rgba(bytes_out);
         if (hipMemcpy(rgba.data(), d_out, bytes_out, hipMemcpyDeviceToHost) != hipSuccess) die("readback failed");
         FILE *f = std::fopen(out.c_str(), "wb");

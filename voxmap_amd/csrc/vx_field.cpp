@@ -169,3 +169,91 @@ int noise_synth(uint32_t seed, int w, int h, uint8_t *out) {
 }
 
 }  // namespace vx
+
+namespace vx {
+
+// ---- 2D mode mesh (sdf.cpp:362-401) --------------------------------------
+// c2d (x fastest, X*Y): the vis colour of each column's top block with z >= 1
+// (sdf.cpp:201-204: z2d starts at 0 and only z > z2d replaces it), 0 where
+// there is none or it is not a meshed index.  Greedy quads per colour
+// c = 1..pal_size-1 in ascending order (sdf.cpp:367; colour 0 never occurs
+// after the remap, air = pal_size is never meshed), cells visited x-major
+// then y (forXY, voxmap.h:45-49), each quad grown along x while the mask
+// holds (:378), then along y while the whole row of w cells holds (:380-385),
+// its cells then cleared (:391-395).  origin[i] = x0 | y0 << 16 of the quad
+// covering cell i (the quad's corner is v_cellPos, render.vert:27).
+void mesh2d(const uint8_t *c2d, int X, int Y, std::vector<Quad2d> &quads, uint32_t *origin) {
+    quads.clear();
+    std::vector<uint8_t> mask((size_t)X * Y);
+    auto at = [&](int x, int y) -> uint8_t & { return mask[(size_t)y * X + x]; };
+    for (int color = 1; color < VX_PAL_SIZE; color++) {
+        bool any = false;
+        for (size_t i = 0; i < mask.size(); i++) any |= (mask[i] = c2d[i] == color) != 0;
+        if (!any) continue;
+        for (int x = 0; x < X; x++)
+            for (int y = 0; y < Y; y++) {
+                if (!at(x, y)) continue;
+                int w = 1, h = 1;
+                while (x + w < X && at(x + w, y)) w++;
+                for (; y + h < Y; h++) {
+                    bool row = true;
+                    for (int k = 0; k < w && row; k++) row = at(x + k, y + h) != 0;
+                    if (!row) break;
+                }
+                quads.push_back({x, y, w, h, color});
+                for (int l = 0; l < h; l++)
+                    for (int k = 0; k < w; k++) {
+                        at(x + k, y + l) = 0;
+                        if (origin) origin[(size_t)(y + l) * X + (x + k)] = (uint32_t)x | ((uint32_t)y << 16);
+                    }
+            }
+    }
+}
+
+// vert2d records (sdf.cpp:154-173): quad2d(x, y, w, 0, 0, h) = tri2d((0,0),
+// (w,0), (0,h)) + tri2d((0,h), (w,0), (w,h)); each vertex i16 x, y, 0, dx, dy,
+// 0, u8 colour, 0, id (2 for glass = pal_size - 1, :388), 0 -- 16 bytes.
+size_t vertex2d_bytes(const std::vector<Quad2d> &quads, uint8_t *out, size_t cap) {
+    const size_t need = quads.size() * 6 * 16;
+    if (!out || cap < need) return need;
+    uint8_t *p = out;
+    auto i16 = [&](int v) { *p++ = (uint8_t)(v & 0xff); *p++ = (uint8_t)((v >> 8) & 0xff); };
+    for (const Quad2d &q : quads) {
+        const int d[6][2] = {{0, 0}, {q.w, 0}, {0, q.h}, {0, q.h}, {q.w, 0}, {q.w, q.h}};
+        for (int v = 0; v < 6; v++) {
+            i16(q.x); i16(q.y); i16(0);
+            i16(d[v][0]); i16(d[v][1]); i16(0);
+            *p++ = (uint8_t)q.color;
+            *p++ = 0;
+            *p++ = (uint8_t)(q.color == VX_GLASS ? 2 : 0);
+            *p++ = 0;
+        }
+    }
+    return need;
+}
+
+}  // namespace vx
+
+extern "C" int vx_vertex2d(const uint8_t *rgba, int X, int Y, int Z, void *out, size_t cap, size_t *out_size) {
+    using namespace vx;
+    if (!rgba || !out_size || X <= 0 || Y <= 0 || Z <= 0 || X > 65535 || Y > 65535)
+        return set_error(VX_EINVAL, "vx_vertex2d: bad arguments");
+    // footprint: each column's top block (R == 0, sdf.cpp:430) with z >= 1 (sdf.cpp:201-204)
+    const size_t n = (size_t)X * Y;
+    std::vector<uint8_t> c2d(n, 0);
+    for (size_t i = 0; i < n; i++)
+        for (int z = Z - 1; z >= 1; z--) {
+            const uint8_t *t = rgba + 4 * (i + n * (size_t)z);
+            if (t[0] == 0) {
+                c2d[i] = (t[2] >= 1 && t[2] < VX_PAL_SIZE) ? t[2] : 0;
+                break;
+            }
+        }
+    std::vector<Quad2d> quads;
+    mesh2d(c2d.data(), X, Y, quads, nullptr);
+    *out_size = vertex2d_bytes(quads, nullptr, 0);
+    if (!out) return VX_OK;
+    if (cap < *out_size) return set_error(VX_EINVAL, "vx_vertex2d: output buffer too small");
+    vertex2d_bytes(quads, static_cast<uint8_t *>(out), cap);
+    return VX_OK;
+}

@@ -3,6 +3,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 #include "../../include/voxmap.h"
 
 namespace vx {
@@ -10,6 +11,8 @@ namespace vx {
 // Error plumbing: every C entry point returns a VX_E* code and leaves a
 // message in a thread-local buffer (vx_last_error).
 int set_error(int code, const std::string &msg);
+// the HIP device ordinal a scene lives on (vx_api.cpp)
+int scene_device(const vx_scene *s);
 
 // One sun direction of the march (render.frag:75-142) with the per-frame
 // constants its loop needs: sign(r), |r|, RN(1/|r|) (Markstein division).
@@ -58,13 +61,16 @@ struct KernelArgs {
     unsigned SXpYp, sunp_texels;
     const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *noise;   // RGBA8 noise texels
+    const uint32_t *fp2d;    // 2D mode: 2 words per column (x fastest): vis colour, quad corner x0 | y0 << 16
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
     float noise_rw, noise_rh;    // 1/noise_w, 1/noise_h (exact)
     int noise_lw;                // log2(noise_w)
     int w, h;                // frame size
-    int tile_size;           // tiled mode: tile edge in pixels (multiple of 16)
-    int tiles_x;             // ceil(w / tile_size)
+    int tile_w, tile_h;      // tiled mode: tile size in pixels (multiples of VX_TILE_ALIGN_X / _Y)
+    int tiles_x;             // ceil(w / tile_w)
+    int tile_pitch;          // tiled mode, compact: row pitch in pixels (tile_w for tiles, w for bands)
+    int tile_inplace;        // tiled mode: 1 = pixels at their frame positions, 0 = compact tile-major
     const int *tile_ids;     // tiled mode: device list of tile ids, else nullptr
     int n_tiles;
     void *out;               // RGBA32F or RGBA8
@@ -85,6 +91,9 @@ struct KernelArgs {
     float kx4, ky;           // 4*(camera padded x), camera padded y (ray octant terms added per lane)
     unsigned kz;             // 4*XpYp*(camera padded z), mod 2^32
 };
+
+// tile sizes must be multiples of the render kernel's block (32 x 8 pixels)
+constexpr int VX_TILE_ALIGN_X = 32, VX_TILE_ALIGN_Y = 8;
 
 void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, int max_steps, FrameConsts &fc);
 
@@ -116,6 +125,15 @@ int launch_field_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t 
                         int Y, int Z, int pad, void *stream);
 // upload's B -> vis colour in place (1..VX_PAL_SIZE-1 kept, else 0), original B into bcol
 int launch_field_vis(uint32_t *lin, uint8_t *bcol, int X, int Y, int Z, void *stream);
+
+// 2D mode (sdf.cpp:362-401; DESIGN.md §3 "2D mode"): the footprint's greedy quads
+struct Quad2d {
+    int x, y, w, h, color;
+};
+void mesh2d(const uint8_t *c2d, int X, int Y, std::vector<Quad2d> &quads, uint32_t *origin);
+size_t vertex2d_bytes(const std::vector<Quad2d> &quads, uint8_t *out, size_t cap);
+// c2d (X*Y, x fastest) of the upload after launch_field_vis: vis colour of each column's top block, z >= 1
+int launch_footprint(const uint32_t *lin, uint8_t *c2d, int X, int Y, int Z, void *stream);
 
 // Launchers (vx_kernels.hip).  Return a hipError_t as int.
 int launch_render(const KernelArgs &a, int pixel_format, void *stream);

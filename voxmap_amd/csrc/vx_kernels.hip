@@ -1016,16 +1016,28 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     return s;
 }
 
+__device__ __forceinline__ uint32_t pack_rgba8(const float rgba[4]) {
+    uint32_t pk = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) pk |= (uint32_t)(gclamp(rgba[i], 0.0f, 1.0f) * 255.0f + 0.5f) << (8 * i);
+    return pk;
+}
+
 template <int FMT>
 __device__ __forceinline__ void store_pixel(const KernelArgs &a, size_t idx, const float rgba[4]) {
-    if (FMT == VX_PIXEL_RGBA32F) {
+    if (FMT == VX_PIXEL_RGBA32F)
         reinterpret_cast<float4 *>(a.out)[idx] = make_float4(rgba[0], rgba[1], rgba[2], rgba[3]);
-    } else {
-        uint32_t pk = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) pk |= (uint32_t)(gclamp(rgba[i], 0.0f, 1.0f) * 255.0f + 0.5f) << (8 * i);
-        reinterpret_cast<uint32_t *>(a.out)[idx] = pk;
-    }
+    else
+        reinterpret_cast<uint32_t *>(a.out)[idx] = pack_rgba8(rgba);
+}
+
+// output index of pixel (px, py), at (x, y) inside tile k of a tiled launch:
+// compact tile-major (tile k at k * tile_h * pitch, rows pitch apart) or,
+// tile_inplace, the pixel's own place in the w-wide frame
+template <bool TILED>
+__device__ __forceinline__ size_t out_index(const KernelArgs &a, int k, int x, int y, int px, int py) {
+    if (TILED && !a.tile_inplace) return (size_t)k * a.tile_h * a.tile_pitch + (size_t)y * a.tile_pitch + x;
+    return (size_t)py * a.w + px;
 }
 
 // view ray of pixel (px, py): nx = (2px+1)/w - 1, ny = 1 - (2py+1)/h with exact quotients
@@ -1045,7 +1057,68 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
     rgba[3] = 1.0f;
 }
 
-// Lane = pixel, wave = 8x8 tile, workgroup = 16x16 pixels.
+// ---------------- 2D mode (u_quality = 0) ----------------
+// drawScene binds the vertex2d mesh when mode == MODE_2D and sets u_quality = 0
+// (render.js:278, 287): the footprint quads of sdf.cpp:362-401 on the z = 0
+// plane (vert2d: normal byte 0 -> v_normal = (1, 0, 0), render.vert:16; id 2
+// for glass), front-facing from above (tri2d winding, culled from below,
+// render.js:88-91), over the clear colour (0.9, 0.9, 0.9) (render.js:274-275:
+// from the second frame on).  render.frag with u_quality = 0 outputs the
+// palette colour (:241-244); glass: alpha 0.8 exp2(dot(rayDir, n)), rgb *=
+// 0.2 atmCol (:246-249), blended over the clear colour.  The march and the
+// AO sample the reference also runs there do not reach the output (:244): not
+// run.  Oracle: vxo_render.c shade_2d.
+constexpr float kClear2d = 0.9f;
+__device__ void shade_2d(const KernelArgs &a, float d0, float d1, float d2, float rgba[4], Counters &cnt,
+                         unsigned &n_sky, unsigned &n_block, unsigned &n_glass) {
+    const FrameConsts &F = a.fc;
+    rgba[0] = rgba[1] = rgba[2] = kClear2d;
+    rgba[3] = 1.0f;
+    const float zr = (float)(0 - F.cam_cell[2]) - F.cam_fract[2];      // the plane, camera-relative
+    int c = 0, x = 0, y = 0;
+    float hx = 0.0f, hy = 0.0f;
+    if (zr < 0.0f && d2 < 0.0f) {                                       // camera above, ray going down
+        const float t = zr / d2;
+        hx = F.cam_fract[0] + t * d0;
+        hy = F.cam_fract[1] + t * d1;
+        x = F.cam_cell[0] + f2i(floorf(hx));
+        y = F.cam_cell[1] + f2i(floorf(hy));
+        if ((unsigned)x < (unsigned)a.X && (unsigned)y < (unsigned)a.Y) {
+            c = (int)a.fp2d[2 * ((size_t)y * a.X + x)];
+            cnt.prim_fetch++;
+        }
+    }
+    if (c == 0) {
+        n_sky = 1;
+        return;
+    }
+    const uint32_t org = a.fp2d[2 * ((size_t)y * a.X + x) + 1];
+    const int x0 = (int)(org & 0xffffu), y0 = (int)(org >> 16);
+    const float pc0 = kPalette[c][0], pc1 = kPalette[c][1], pc2 = kPalette[c][2];
+    if (c != kGlass) {
+        n_block = 1;
+        rgba[0] = pc0; rgba[1] = pc1; rgba[2] = pc2;
+        return;
+    }
+    n_glass = 1;
+    // v_cellPos = the quad corner (x0, y0, 0), v_fractPos = hit - corner (render.vert:27-28)
+    const float f0 = (float)(F.cam_cell[0] - x0) + hx, f1 = (float)(F.cam_cell[1] - y0) + hy;
+    float r0, r1, r2;
+    normalize3((float)(x0 - F.cam_cell[0]) + (f0 - F.cam_fract[0]), (float)(y0 - F.cam_cell[1]) + (f1 - F.cam_fract[1]),
+               (float)(0 - F.cam_cell[2]) + (0.0f - F.cam_fract[2]), r0, r1, r2);     // render.frag:154
+    const float k = 2.0f * ((1.0f * r0 + 0.0f * r1) + 0.0f * r2);                  // reflect(rayDir, n)
+    const float rz = sqrtf(gmax(0.0f, r2 - k * 0.0f));
+    const float al = 0.8f * vexp2((r0 * 1.0f + r1 * 0.0f) + r2 * 0.0f);
+    const float pc[3] = {pc0, pc1, pc2};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float atm = gmix(F.scatterCol[i], F.spaceCol[i], rz);
+        const float src = pc[i] * (0.2f * atm);
+        rgba[i] = src * al + kClear2d * (1.0f - al);
+    }
+}
+
+// Lane = pixel, wave = 8x8 tile, workgroup = 32x8 pixels.
 // EXT: 0 = v1 (the reference's shader), 1 = extensions (REFLECT, ROUGH) with
 // the hard shadow, 2 = extensions with soft shadows (n sun samples).  Each
 // instantiation carries only its own code and registers; soft shadows in a
@@ -1063,15 +1136,24 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
 #else
 #define VX_OCC_ATTR
 #endif
-// Workgroup = VX_WG threads: 256 (four 8x8-pixel waves, a 16x16 tile), 64
-// (one wave, an 8x8 tile) or 1024 (sixteen waves, a 32x32 tile).
-#ifndef VX_WG
-#define VX_WG 256
+// Workgroup = 256 threads = four 8x8-pixel waves side by side: a 32x8 pixel
+// block (VX_BX = 32; 16 gives the round-1 16x16 block).  A 32-pixel block row
+// is 128 B of RGBA8: the framebuffer store goes through LDS so every wave
+// writes two whole 128-B rows (full cache lines) instead of eight 32-B
+// pieces of its own 8x8 tile (VX_STAGE).
+#ifndef VX_BX
+#define VX_BX 32
 #endif
-constexpr int kWG = VX_WG;
-constexpr int kBE = kWG == 1024 ? 32 : (kWG == 256 ? 16 : 8);   // block edge in pixels
-constexpr int kBS = kWG == 1024 ? 5 : (kWG == 256 ? 4 : 3);      // log2(kBE)
-constexpr int kWX = kBE / 8;                                       // waves per block row
+#ifndef VX_STAGE
+#define VX_STAGE 1
+#endif
+constexpr int kWG = 256;
+constexpr int kBX = VX_BX;                 // block width in pixels (16 or 32)
+constexpr int kBY = kWG / kBX;             // block height
+constexpr int kBXS = kBX == 32 ? 5 : 4;    // log2(kBX)
+constexpr int kBYS = kBY == 8 ? 3 : 4;     // log2(kBY)
+constexpr int kWX = kBX / 8;               // waves per block row
+static_assert(kBX == 16 || kBX == 32, "VX_BX must be 16 or 32");
 
 // F32IDX: the fp32 primary index (a.prim_f32) -- a kernel of its own: two
 // inlined primary() copies in one kernel make the compiler copy KernelArgs
@@ -1083,6 +1165,7 @@ void k_render(KernelArgs a) {
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     __shared__ float4 s_lds[64 + 128];
+    __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
     float *s_unorm = reinterpret_cast<float *>(s_lds);
 #pragma unroll
     for (int i = threadIdx.x; i < 256; i += kWG)        // = (float)i / 255.0f, the IEEE quotient (§5)
@@ -1098,18 +1181,21 @@ void k_render(KernelArgs a) {
     const int ly = ((wave / kWX) << 3) | (lane >> 3);
     int ox, oy, tx0 = 0, ty0 = 0, tile_k = 0;
     if (TILED) {
-        const int per = a.tile_size >> kBS;
-        const int bpt = per * per;
+        // tiles of tile_w x tile_h pixels (multiples of the block), tile k of the
+        // list at k * tile_w * tile_h in the compact output (or at its own
+        // place in a w-wide frame: tile_inplace)
+        const int perx = a.tile_w >> kBXS, pery = a.tile_h >> kBYS;
+        const int bpt = perx * pery;
         tile_k = blockIdx.x / bpt;
         const int sub = blockIdx.x % bpt;
         const int tid = a.tile_ids[tile_k];
-        tx0 = (sub % per) << kBS;
-        ty0 = (sub / per) << kBS;
-        ox = (tid % a.tiles_x) * a.tile_size + tx0;
-        oy = (tid / a.tiles_x) * a.tile_size + ty0;
+        tx0 = (sub % perx) << kBXS;
+        ty0 = (sub / perx) << kBYS;
+        ox = (tid % a.tiles_x) * a.tile_w + tx0;
+        oy = (tid / a.tiles_x) * a.tile_h + ty0;
     } else {
-        ox = blockIdx.x << kBS;
-        oy = blockIdx.y << kBS;
+        ox = blockIdx.x << kBXS;
+        oy = blockIdx.y << kBYS;
     }
     const int px = ox + lx, py = oy + ly;
     const FrameConsts &F = a.fc;
@@ -1158,11 +1244,21 @@ void k_render(KernelArgs a) {
             }
         }
         rgba[3] = 1.0f;
-        const size_t idx = TILED ? (size_t)tile_k * a.tile_size * a.tile_size + (size_t)(ty0 + ly) * a.tile_size +
-                                       (tx0 + lx)
-                                 : (size_t)py * a.w + px;
-        store_pixel<FMT>(a, idx, rgba);
+        if (FMT == VX_PIXEL_RGBA8 && VX_STAGE) {
+            s_px[ly][lx] = pack_rgba8(rgba);
+        } else {
+            store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
+        }
         n_px = 1;
+    }
+    if (FMT == VX_PIXEL_RGBA8 && VX_STAGE) {
+        // block -> framebuffer in whole rows: thread t stores pixel (t % kBX, t / kBX)
+        // of the block, so a wave writes two contiguous kBX*4-byte rows
+        __syncthreads();
+        const int sx = threadIdx.x & (kBX - 1), sy = threadIdx.x >> kBXS;
+        if (ox + sx < a.w && oy + sy < a.h)
+            reinterpret_cast<uint32_t *>(a.out)[out_index<TILED>(a, tile_k, tx0 + sx, ty0 + sy, ox + sx, oy + sy)] =
+                s_px[sy][sx];
     }
     if (STATS) {
         unsigned long long v[ST_COUNT];
@@ -1186,6 +1282,66 @@ void k_render(KernelArgs a) {
             unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
 #pragma unroll
             for (int i = 0; i < ST_COUNT; i++) atomicAdd(row + i, v[i]);
+        }
+    }
+}
+
+// 2D mode frames (quality 0) in a kernel of their own: the 3D kernel keeps its
+// code and registers (a third user of the frame constants in k_render made
+// the compiler copy KernelArgs to scratch).  Same pixel mapping and stores.
+template <int FMT, bool STATS, bool TILED>
+__global__ __launch_bounds__(kWG) void k_render_2d(KernelArgs a) {
+    __shared__ uint32_t s_px[kBY][kBX];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lx = ((wave % kWX) << 3) | (lane & 7);
+    const int ly = ((wave / kWX) << 3) | (lane >> 3);
+    int ox, oy, tx0 = 0, ty0 = 0, tile_k = 0;
+    if (TILED) {
+        const int perx = a.tile_w >> kBXS, pery = a.tile_h >> kBYS;
+        const int bpt = perx * pery;
+        tile_k = blockIdx.x / bpt;
+        const int sub = blockIdx.x % bpt;
+        const int tid = a.tile_ids[tile_k];
+        tx0 = (sub % perx) << kBXS;
+        ty0 = (sub / perx) << kBYS;
+        ox = (tid % a.tiles_x) * a.tile_w + tx0;
+        oy = (tid / a.tiles_x) * a.tile_h + ty0;
+    } else {
+        ox = blockIdx.x << kBXS;
+        oy = blockIdx.y << kBYS;
+    }
+    const int px = ox + lx, py = oy + ly;
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
+    if (px < a.w && py < a.h) {
+        float d0, d1, d2, rgba[4];
+        view_ray(a.fc, px, py, d0, d1, d2);
+        shade_2d(a, d0, d1, d2, rgba, cnt, n_sky, n_block, n_glass);
+        if (FMT == VX_PIXEL_RGBA8 && VX_STAGE)
+            s_px[ly][lx] = pack_rgba8(rgba);
+        else
+            store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
+        n_px = 1;
+    }
+    if (FMT == VX_PIXEL_RGBA8 && VX_STAGE) {
+        __syncthreads();
+        const int sx = threadIdx.x & (kBX - 1), sy = threadIdx.x >> kBXS;
+        if (ox + sx < a.w && oy + sy < a.h)
+            reinterpret_cast<uint32_t *>(a.out)[out_index<TILED>(a, tile_k, tx0 + sx, ty0 + sy, ox + sx, oy + sy)] =
+                s_px[sy][sx];
+    }
+    if (STATS) {
+        unsigned long long v[ST_COUNT] = {};
+        v[ST_PIXELS] = wave_sum(n_px);
+        v[ST_SKY] = wave_sum(n_sky);
+        v[ST_BLOCK] = wave_sum(n_block);
+        v[ST_GLASS] = wave_sum(n_glass);
+        v[ST_PRIM_FETCH] = wave_sum(cnt.prim_fetch);
+        if (lane == 0) {
+            unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
+#pragma unroll
+            for (int i = 0; i < ST_COUNT; i++)
+                if (v[i]) atomicAdd(row + i, v[i]);
         }
     }
 }
@@ -1262,8 +1418,18 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
     const bool tiled = a.tile_ids != nullptr;
     const bool st = a.stats != nullptr;
     dim3 block(kWG);
-    dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_size >> kBS) * (a.tile_size >> kBS))
-                      : dim3((a.w + kBE - 1) / kBE, (a.h + kBE - 1) / kBE);
+    dim3 grid = tiled ? dim3(a.n_tiles * (a.tile_w >> kBXS) * (a.tile_h >> kBYS))
+                      : dim3((a.w + kBX - 1) / kBX, (a.h + kBY - 1) / kBY);
+    if (a.fc.quality == 0) {          // MODE_2D: the vertex2d mesh (render.js:278, 287)
+#define VX_L2(F, S, T) hipLaunchKernelGGL((k_render_2d<F, S, T>), grid, block, 0, s, a)
+#define VX_L2T(F, S) do { if (tiled) VX_L2(F, S, true); else VX_L2(F, S, false); } while (0)
+        if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_L2T(0, true); else VX_L2T(0, false); }
+        else { if (st) VX_L2T(1, true); else VX_L2T(1, false); }
+#undef VX_L2T
+#undef VX_L2
+        if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
+        return (int)hipGetLastError();
+    }
     const int ext = a.fc.n_sun > 1 ? 2 : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
 #define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
 #define VX_LE(F, S, T) do { if (ext == 2) VX_L(F, S, T, 2); else if (ext) VX_L(F, S, T, 1); else VX_L(F, S, T, 0); } while (0)
@@ -1402,6 +1568,21 @@ __global__ void k_vis(uint32_t *lin, uint8_t *bcol, size_t N) {
     const uint32_t v = b - 1u < (uint32_t)(VX_PAL_SIZE - 1) ? b : 0u;
     lin[i] = (t & 0xff00ffffu) | (v << 16);
 }
+// 2D mode footprint (sdf.cpp:201-204, 235-239): per column the vis colour of
+// the top block with z >= 1 (a block is R == 0, sdf.cpp:430), else 0
+__global__ void k_footprint(const uint32_t *lin, uint8_t *c2d, int X, int Y, int Z) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)X * Y) return;
+    uint8_t c = 0;
+    for (int z = Z - 1; z >= 1; z--) {
+        const uint32_t t = lin[i + (size_t)X * Y * z];
+        if ((t & 0xffu) == 0) {
+            c = (uint8_t)((t >> 16) & 0xffu);
+            break;
+        }
+    }
+    c2d[i] = c;
+}
 // One octant copy, linear: RGBA (R, G from rg; B = map.bin's B from bcol; A =
 // the cube size = min(ex, ey, ez), since the box grows from the largest cube)
 // for vx_scene_read_field_copy, or the raw texels (rg == nullptr: vis colour,
@@ -1470,6 +1651,13 @@ int launch_field_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t 
     const size_t N = (size_t)X * Y * Z;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, bcol,
                        prim_copy, out, X, Y, Z, pad);
+    return (int)hipGetLastError();
+}
+
+int launch_footprint(const uint32_t *lin, uint8_t *c2d, int X, int Y, int Z, void *stream) {
+    const size_t N = (size_t)X * Y;
+    hipLaunchKernelGGL(k_footprint, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lin, c2d,
+                       X, Y, Z);
     return (int)hipGetLastError();
 }
 

@@ -1,104 +1,69 @@
-"""Screen-space sharding of one frame across GPUs.
+"""Screen-space sharding of one frame across GPUs — the
+host-side mirror of the native path (vx_mgpu_*, csrc/vx_mgpu.cpp).
 
 Pixels are independent (render.frag reads only the replicated field and noise
-textures), so a frame is cut into square tiles dealt round-robin to ranks —
-interleaving balances cheap sky tiles against expensive geometry tiles.  Each
-rank renders its tiles into a compact tile-major buffer (vx_render_tiles);
-rank 0 gathers the buffers with one collective (torch.distributed.gather, RCCL
-over xGMI on MI355X nodes, gloo in CPU tests) and scatters them into the frame
-(vx_detile).  There is no other exchange.
+textures), so a frame is cut into full-width bands of ``band_rows`` rows,
+dealt round-robin (band b -> rank b % world; neighbouring bands cost about the
+same, so the interleave balances cheap sky against expensive geometry).  Every
+rank renders its bands in place in its own w x h frame; rank 0 receives every
+other rank's bands straight into the same rows of its frame with one batch of
+point-to-point transfers.  A band is contiguous in a row-major frame, so there
+is no tile-major staging buffer, no concatenation and no de-tile pass.
 
-Gather sizes must match across ranks, so every rank's list is padded to the
-longest one by repeating its last tile (the repeat re-writes identical pixels).
+``BandGather`` runs that protocol over torch.distributed (gloo in the CPU
+tests, "nccl" = RCCL with ``bench.py --gather torch``); the product path for
+GPUs is the native vx_mgpu_render (bench.py default), which issues the same
+transfers as one RCCL group from C++.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
 
-import numpy as np
-
-
-@dataclass(frozen=True)
-class TileLayout:
-    width: int
-    height: int
-    tile: int
-
-    @property
-    def tiles_x(self) -> int:
-        return -(-self.width // self.tile)
-
-    @property
-    def tiles_y(self) -> int:
-        return -(-self.height // self.tile)
-
-    @property
-    def n_tiles(self) -> int:
-        return self.tiles_x * self.tiles_y
-
-    def rank_tiles(self, world: int, rank: int) -> list:
-        """Round-robin deal (tile t -> rank t % world)."""
-        return list(range(rank, self.n_tiles, world))
-
-    def padded(self, world: int):
-        """(per-rank padded lists, their concatenation in rank order, tiles per rank)."""
-        lists = [self.rank_tiles(world, r) for r in range(world)]
-        per = max(len(l) for l in lists)
-        if per == 0:
-            raise ValueError("frame has no tiles")
-        padded = []
-        for l in lists:
-            if not l:            # more ranks than tiles: repeat tile 0 (rewrites identical pixels)
-                l = [0]
-            padded.append(l + [l[-1]] * (per - len(l)))
-        concat = [t for l in padded for t in l]
-        return padded, concat, per
+def n_bands(h: int, band_rows: int) -> int:
+    return -(-h // band_rows)
 
 
-def detile_host(tiles: np.ndarray, layout: TileLayout, ids) -> np.ndarray:
-    """Host twin of vx_detile for CPU checks: tiles (n, ts, ts, C) -> frame (h, w, C)."""
-    ts = layout.tile
-    frame = np.zeros((layout.height, layout.width, tiles.shape[-1]), tiles.dtype)
-    for k, t in enumerate(ids):
-        x0, y0 = (t % layout.tiles_x) * ts, (t // layout.tiles_x) * ts
-        h = min(ts, layout.height - y0)
-        w = min(ts, layout.width - x0)
-        frame[y0:y0 + h, x0:x0 + w] = tiles[k, :h, :w]
-    return frame
+def bands(h: int, band_rows: int, world: int, rank: int) -> list:
+    """Band ids of ``rank`` (vx_mgpu_bands): b = rank, rank + world, ..."""
+    return list(range(rank, n_bands(h, band_rows), world))
 
 
-class ShardedFrame:
-    """One rank's part of a sharded frame: render my tiles, gather to rank 0, de-tile.
+def band_rows_of(b: int, h: int, band_rows: int) -> slice:
+    return slice(b * band_rows, min(h, (b + 1) * band_rows))
 
-    ``render_tiles(ids, out_tensor)`` and ``detile(concat_ids, tiles_tensor, frame_tensor)``
-    are injected: on GPUs they are Scene.render_tiles / Scene.detile over device tensors;
-    CPU tests pass host stand-ins.  ``dist`` is torch.distributed (initialised).
+
+class BandGather:
+    """One rank's part of a sharded frame: render my bands in place, gather to rank 0.
+
+    ``render_bands(ids, frame)`` is injected: on GPUs Scene.render_bands(inplace=True)
+    into the frame tensor; CPU tests pass a host stand-in.  ``dist`` is an
+    initialised torch.distributed.
     """
 
-    def __init__(self, dist, layout: TileLayout, channels: int, dtype, device, render_tiles, detile):
+    def __init__(self, dist, w: int, h: int, band_rows: int, channels: int, dtype, device, render_bands):
         import torch
         self.dist = dist
-        self.layout = layout
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
-        lists, self.concat, self.per = layout.padded(self.world)
-        self.mine = lists[self.rank]
-        ts = layout.tile
-        self.buf = torch.empty((self.per, ts, ts, channels), dtype=dtype, device=device)
-        if self.rank == 0:
-            self.parts = [torch.empty_like(self.buf) for _ in range(self.world)]
-            self.cat = torch.empty((self.world * self.per, ts, ts, channels), dtype=dtype, device=device)
-            self.frame = torch.empty((layout.height, layout.width, channels), dtype=dtype, device=device)
-        else:
-            self.parts = self.cat = self.frame = None
-        self._render = render_tiles
-        self._detile = detile
+        self.w, self.h, self.band_rows = w, h, band_rows
+        self.mine = bands(h, band_rows, self.world, self.rank)
+        self.frame = torch.empty((h, w, channels), dtype=dtype, device=device)
+        self._render = render_bands
+
+    def transfers(self):
+        """(band id, owner) of every band that moves (owner != 0)."""
+        return [(b, b % self.world) for b in range(n_bands(self.h, self.band_rows)) if b % self.world != 0]
 
     def step(self):
-        import torch
-        self._render(self.mine, self.buf)
-        self.dist.gather(self.buf, gather_list=self.parts, dst=0)
-        if self.rank == 0:
-            torch.cat(self.parts, out=self.cat)
-            self._detile(self.concat, self.cat, self.frame)
-        return self.frame
+        if self.mine:
+            self._render(self.mine, self.frame)
+        ops = []
+        for b, owner in self.transfers():
+            rows = self.frame[band_rows_of(b, self.h, self.band_rows)]
+            if self.rank == 0:
+                ops.append(self.dist.P2POp(self.dist.irecv, rows, owner))
+            elif owner == self.rank:
+                ops.append(self.dist.P2POp(self.dist.isend, rows, 0))
+        if ops:
+            for req in self.dist.batch_isend_irecv(ops):
+                req.wait()
+        return self.frame if self.rank == 0 else None

@@ -160,6 +160,14 @@ class Scene:
         check(lib().vx_scene_read_field_copy(self.handle, octant, out.ctypes.data, out.nbytes))
         return out
 
+    def vertex2d(self) -> bytes:
+        """The 2D mode mesh as vertex2d.bin bytes (sdf.cpp:362-401, vx_scene_vertex2d)."""
+        n = C.c_size_t()
+        check(lib().vx_scene_vertex2d(self.handle, None, 0, C.byref(n)))
+        out = np.empty(n.value, np.uint8)
+        check(lib().vx_scene_vertex2d(self.handle, out.ctypes.data, out.size, C.byref(n)))
+        return out.tobytes()
+
     def read_boxes(self, octant: int = 0) -> np.ndarray:
         """(Z, Y, X, 4) uint8: colour, ex, ey, ez of the octant's traversal boxes."""
         X, Y, Z = self.dims
@@ -198,6 +206,17 @@ class Scene:
                                     C.byref(st) if st is not None else None))
         return st
 
+    def render_bands(self, frame: Frame, band_rows: int, band_ids, out_ptr: int, *, inplace: bool = True,
+                     pixel_format=_abi.PIXEL_RGBA8, stream=None, stats: bool = False):
+        """Full-width bands of rows (vx_render_bands): in place in a w*h frame, or compact."""
+        ids = np.ascontiguousarray(np.asarray(band_ids, dtype=np.int32))
+        st = Stats() if stats else None
+        check(lib().vx_render_bands(self.handle, C.byref(frame.params), frame.width, frame.height, int(band_rows),
+                                    ids.ctypes.data_as(C.POINTER(C.c_int)), int(ids.size), pixel_format,
+                                    C.c_void_p(out_ptr), 1 if inplace else 0,
+                                    C.c_void_p(stream) if stream else None, C.byref(st) if st is not None else None))
+        return st
+
     def detile(self, w, h, tile_size, tile_ids, tiles_ptr, frame_ptr, *, pixel_format=_abi.PIXEL_RGBA8,
                stream=None):
         ids = np.ascontiguousarray(np.asarray(tile_ids, dtype=np.int32))
@@ -218,6 +237,55 @@ class Scene:
         return img
 
 
+def mgpu_unique_id() -> bytes:
+    """Rank 0: the RCCL unique id (VX_MGPU_UID_BYTES) every rank passes to MultiGPU."""
+    buf = (C.c_char * _abi.MGPU_UID_BYTES)()
+    check(lib().vx_mgpu_unique_id(buf))
+    return bytes(buf)
+
+
+def mgpu_bands(h: int, band_rows: int, nranks: int, rank: int) -> list:
+    """The band deal of vx_mgpu_render (band b -> rank b % nranks)."""
+    n = lib().vx_mgpu_bands(int(h), int(band_rows), int(nranks), int(rank), None, 0)
+    if n < 0:
+        check(n)
+    ids = (C.c_int * max(n, 1))()
+    lib().vx_mgpu_bands(int(h), int(band_rows), int(nranks), int(rank), ids, n)
+    return list(ids[:n])
+
+
+class MultiGPU:
+    """One rank of a frame shared by the GPUs of a node (vx_mgpu_*: bands
+    rendered in place, gathered into rank 0's frame over RCCL)."""
+
+    def __init__(self, scene: Scene, uid: bytes, nranks: int, rank: int):
+        h = C.c_void_p()
+        buf = (C.c_char * _abi.MGPU_UID_BYTES).from_buffer_copy(uid)
+        check(lib().vx_mgpu_create(scene.handle, buf, int(nranks), int(rank), C.byref(h)))
+        self._h = h
+        self.scene = scene
+        self.nranks, self.rank = int(nranks), int(rank)
+
+    def render(self, frame: Frame, band_rows: int, frame_ptr: int, *, pixel_format=_abi.PIXEL_RGBA8, stream=None,
+               stats: bool = False):
+        st = Stats() if stats else None
+        check(lib().vx_mgpu_render(self._h, C.byref(frame.params), frame.width, frame.height, int(band_rows),
+                                   pixel_format, C.c_void_p(frame_ptr), C.c_void_p(stream) if stream else None,
+                                   C.byref(st) if st is not None else None))
+        return st
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().vx_mgpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ---- host helpers over the ABI ------------------------------------------------
 
 def field_build(color_zyx: np.ndarray, n_threads: int = 0) -> np.ndarray:
@@ -236,6 +304,17 @@ def field_build_gpu(color_zyx: np.ndarray, device: int = 0) -> np.ndarray:
     out = np.empty((Z, Y, X, 4), np.uint8)
     check(lib().vx_field_build_gpu(col.ctypes.data, X, Y, Z, out.ctypes.data, int(device)))
     return out
+
+
+def vertex2d(field_zyx4: np.ndarray) -> bytes:
+    """vertex2d.bin bytes (sdf.cpp:362-401) of a map.bin field (vx_vertex2d, host C++)."""
+    f = np.ascontiguousarray(field_zyx4, dtype=np.uint8)
+    Z, Y, X, _ = f.shape
+    n = C.c_size_t()
+    check(lib().vx_vertex2d(f.ctypes.data, X, Y, Z, None, 0, C.byref(n)))
+    out = np.empty(n.value, np.uint8)
+    check(lib().vx_vertex2d(f.ctypes.data, X, Y, Z, out.ctypes.data, out.size, C.byref(n)))
+    return out.tobytes()
 
 
 def noise_synth(seed: int = 0, w: int = 1024, h: int = 1024) -> np.ndarray:
