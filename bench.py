@@ -213,10 +213,24 @@ def main():
         streams = [torch.cuda.Stream() for _ in range(K)]
         torch.cuda.set_stream(streams[0])
         frames = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(K)]
+        group = None
         if args.gather == "native":
             uid = [vx.mgpu_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            mg = vx.MultiGPU(scene, uid[0], world, rank)
+            try:
+                mg = vx.MultiGPU(scene, uid[0], world, rank)
+                ok = torch.tensor([1])
+            except Exception as e:          # RCCL init refused: fall back to the torch-driven gather
+                print(f"rank {rank}: vx_mgpu_create failed ({e}); falling back to --gather torch", file=sys.stderr)
+                mg, ok = None, torch.tensor([0])
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                if mg is not None:
+                    mg.close()
+                    mg = None
+                args.gather = "torch-fallback"
+                group = dist.new_group(list(range(world)), backend="nccl")
+        if args.gather == "native":
             fns = [(lambda fb=frames[j], sj=streams[j].cuda_stream:
                     mg.render(frame, BAND, fb.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
             st = mg.render(frame, BAND, frames[0].data_ptr(), pixel_format=vx.PIXEL_RGBA8,
@@ -229,7 +243,7 @@ def main():
                 sj = streams[j].cuda_stream
                 g = BandGather(dist, W, H, BAND, 4, torch.uint8, "cuda",
                                lambda ids, fr, sj=sj: scene.render_bands(frame, BAND, ids, fr.data_ptr(),
-                                                                         inplace=True, stream=sj))
+                                                                         inplace=True, stream=sj), group=group)
                 g.frame = frames[j]
                 gs.append(g)
 
@@ -241,7 +255,8 @@ def main():
             fns = [mk(j) for j in range(K)]
             st = scene.render_bands(frame, BAND, gs[0].mine, frames[0].data_ptr(), inplace=True,
                                     stream=streams[0].cuda_stream, stats=True)
-            gather_desc = "torch.distributed batch_isend_irecv (RCCL) into rank 0's frame rows"
+            gather_desc = ("torch.distributed batch_isend_irecv (RCCL) into rank 0's frame rows" +
+                           (" (fallback: vx_mgpu_create failed)" if group is not None else ""))
         keys = [k for k in st.as_dict().keys() if k != "kernel_ms"]
         vec = torch.tensor([float(st.as_dict()[k]) for k in keys], dtype=torch.float64)
         if args.gather == "torch":

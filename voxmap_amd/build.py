@@ -19,7 +19,13 @@ SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_mgp
 ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
 # -fno-slp-vectorize: packed FP32 (v_pk_*) issues at the cost of two scalar ops
 # on gfx950 (profiles/r01_valu_costs.txt), so SLP packing only adds moves.
-FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", f"--offload-arch={ARCH}"]
+# -instcombine-max-copied-from-constant-users: the render kernels take KernelArgs
+# by value and read it through ~300+ pointers; past LLVM's default limit (300)
+# InstCombine stops replacing the kernel's private copy of the arguments by the
+# kernarg segment itself and every lane copies 1.5 KB to scratch
+# (kernel_meta.check catches that).  A speed flag: no effect on fp32 results.
+FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall",
+         "-mllvm", "-instcombine-max-copied-from-constant-users=4000", f"--offload-arch={ARCH}"]
 LIBS = ["-lz", "-lcrypto", "-lpthread", "-lrccl"]
 
 

@@ -39,9 +39,10 @@ class BandGather:
     initialised torch.distributed.
     """
 
-    def __init__(self, dist, w: int, h: int, band_rows: int, channels: int, dtype, device, render_bands):
+    def __init__(self, dist, w: int, h: int, band_rows: int, channels: int, dtype, device, render_bands, group=None):
         import torch
         self.dist = dist
+        self.group = group
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
         self.w, self.h, self.band_rows = w, h, band_rows
@@ -60,9 +61,9 @@ class BandGather:
         for b, owner in self.transfers():
             rows = self.frame[band_rows_of(b, self.h, self.band_rows)]
             if self.rank == 0:
-                ops.append(self.dist.P2POp(self.dist.irecv, rows, owner))
+                ops.append(self.dist.P2POp(self.dist.irecv, rows, owner, self.group))
             elif owner == self.rank:
-                ops.append(self.dist.P2POp(self.dist.isend, rows, 0))
+                ops.append(self.dist.P2POp(self.dist.isend, rows, 0, self.group))
         if ops:
             for req in self.dist.batch_isend_irecv(ops):
                 req.wait()
