@@ -246,7 +246,10 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         if (!lrc) lrc = launch_field_psum(lin, psum, X, Y, Z, s->stream);
         // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
         // march's loaded value carries the exit test (vx_kernels.hip march_fast); values <= Z <= 126
-        if (!lrc && Z <= 126 && max_rg <= Z && (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2)) < (1u << 24)) {
+        const size_t sxy = (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2));
+        // the march's byte offset is 0x4B000000 + x + Xp*y + XpYp*z from fp32 bit patterns
+        // (vx_kernels.hip march_pad): the padded plane below 2^23, the sum below 2^32
+        if (!lrc && Z <= 126 && max_rg <= Z && sxy < (1u << 23) && sxy * (Z + 2 * (Z + 2)) + 0x4B000000u < (1ull << 32)) {
             s->SB = Z + 2;
             s->SXp = X + 2 * s->SB; s->SYp = Y + 2 * s->SB; s->SZp = Z + 2 * s->SB;
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
@@ -434,7 +437,8 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
         // 32-bit byte offsets all 8 copies below 4 GiB
         const double xy4 = 4.0 * (double)s->L.Xp * (double)s->L.Yp;
         const bool ok = xy4 < 8388608.0 && 32.0 * (double)s->L.texels < 4294967296.0 &&
-                        std::abs(p->cam_cell[0]) < (1 << 21) && std::abs(p->cam_cell[1]) < (1 << 21);
+                        std::abs(p->cam_cell[0]) < (1 << 21) && std::abs(p->cam_cell[1]) < (1 << 21) &&
+                        std::abs(p->cam_cell[2]) < (1 << 20) && s->L.Zp < (1 << 20);   // |z| < 2^21 (k_render)
         a.prim_f32 = ok && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
         a.kx4 = (float)(4 * (p->cam_cell[0] + s->L.pad));
         a.ky = (float)(p->cam_cell[1] + s->L.pad);

@@ -56,6 +56,7 @@
 namespace vx {
 namespace {
 
+constexpr int kWG = 256;      // threads per render workgroup (4 waves)
 constexpr int kGlass = 21;  // render.vert:21, sdf.cpp:337
 constexpr float kInf = __builtin_inff();
 
@@ -151,6 +152,11 @@ struct Counters {
 
 // (float)((t >> 8k) & 0xff) as one v_cvt_f32_ubyteK (left to itself the
 // compiler may fold the mask away and emit a shift + convert)
+__device__ __forceinline__ float cvt_f32_ubyte0(uint32_t t) {
+    float r;
+    asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
 __device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(t));
@@ -301,7 +307,7 @@ __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *
 // same fp32 products r*safe of :118 for every possible safe, indexed by the
 // loaded texel -- one ds_read_b128 instead of three multiplies and the
 // byte -> float convert.  nullptr: multiply in the loop (soft-shadow samples).
-template <int SG>   // -1: signs at run time; else the sun's axis signs (march_len_sg)
+template <int SG, bool TAB>   // SG -1: signs at run time; else the sun's axis signs (march_len_sg)
 __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
                                           int c2, float f0, float f1, float f2, unsigned &fetches, unsigned &witers,
                                           const float4 *rstep) {
@@ -310,7 +316,17 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     const int maxs = F.max_steps;
     if (maxs <= 0) return maxs == 0;
     const float xpf = (float)a.SXp;
-    float e0 = (float)(c0 + a.SB), e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB);
+    // Cells as fp32 integers, x and z biased by 2^23 (exact below 2^24): the
+    // bit pattern of 2^23 + n is 0x4B000000 + n, so the x + Xp*y part of the
+    // offset is the bit pattern of one exact fma and the low 24 bits of the z
+    // pattern are z itself -- no float -> int converts in the loop:
+    //   bits(fma(y, Xp, 2^23 + x)) + u24(bits(2^23 + z)) * XpYp
+    //     = 0x4B000000 + x + Xp*y + XpYp*z,
+    // read from the channel base moved down by 0x4B000000 (vx_scene_create
+    // checks Xp*Yp < 2^23 and the sum < 2^32).
+    constexpr float kBias = 8388608.0f;
+    float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB) + kBias;
+    const int8_t *sunb = sun - 0x4B000000;   // (pointer arithmetic: keeps the global address space)
     float len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));
     const unsigned sxpyp = a.SXpYp;
     int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
@@ -318,11 +334,11 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
 #define VX_PAD_STEP(T)                                                                        \
     {                                                                                         \
         float m0, m1, m2;                                                                     \
-        if (rstep) {                                                                          \
+        if (TAB) {                                                                            \
             const float4 q = rstep[tv];                                                       \
             m0 = q.x; m1 = q.y; m2 = q.z;                                                     \
         } else {                                                                              \
-            const float safe = (float)tv;                                                     \
+            const float safe = cvt_f32_ubyte0((uint32_t)tv); /* 1..126 in the loop */          \
             m0 = r0 * safe; m1 = r1 * safe; m2 = r2 * safe;                                   \
         }                                                                                     \
         f0 = f0 + m0 * len; /* :118 */                                                        \
@@ -331,8 +347,9 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
         const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);                     \
         e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                                   \
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2; /* :120 */                               \
-        const unsigned xy = (unsigned)__builtin_fmaf(e1, xpf, e0); /* exact: < 2^24 */        \
-        T = sun[__umul24((unsigned)e2, sxpyp) + xy]; /* :123-128 */                           \
+        const unsigned off = __umul24(__float_as_uint(e2), sxpyp) +                           \
+                             __float_as_uint(__builtin_fmaf(e1, xpf, e0));                    \
+        T = ld_off(sunb, off); /* :123-128 */                                                 \
         fetches += T >= 0 ? 1u : 0u;                                                          \
     }
     int step = 0;                                                                // wave-uniform
@@ -399,23 +416,23 @@ __device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_
 // S by value: the soft-shadow loop indexes sun_k[k] dynamically, and a
 // reference into the kernel argument there made the compiler copy the whole
 // KernelArgs (1.5 KB) to scratch.
+template <bool TAB>   // rstep points at an r*safe table of S (else the loop multiplies)
 __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
                                           float f1, float f2, unsigned &fetches, unsigned &witers,
                                           const float4 *rstep = nullptr) {
     if (VX_MARCH_PAD && S.fast && a.sunp) {
         const int8_t *ch = S.up ? a.sunp : a.sunp + a.sunp_texels;
-        const float4 *rs = VX_RSTEP ? rstep : nullptr;
 #if VX_MARCH_SG
         // wave-uniform switch on the frame's sun signs: one specialised loop each
         const int sg = (S.sign[0] > 0.0f ? 1 : 0) | (S.sign[1] > 0.0f ? 2 : 0) | (S.sign[2] > 0.0f ? 4 : 0);
         switch (sg) {
-#define VX_SG(K) case K: return march_pad<K>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rs);
+#define VX_SG(K) case K: return march_pad<K, TAB>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rstep);
             VX_SG(0) VX_SG(1) VX_SG(2) VX_SG(3) VX_SG(4) VX_SG(5) VX_SG(6)
-            default: return march_pad<7>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rs);
+            default: return march_pad<7, TAB>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rstep);
 #undef VX_SG
         }
 #else
-        return march_pad<-1>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rs);
+        return march_pad<-1, TAB>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rstep);
 #endif
     }
     const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
@@ -483,16 +500,19 @@ __device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d
     const uint32_t *ppad = a.prim + (size_t)oct * a.copy_texels;
     const int kray = (int)a.kcam - ip0 - a.Xp * ip1 - (int)a.XpYp * ip2;
     // F32IDX (a.prim_f32): the byte offset 4*(x + Xp*y) in fp32 (exact, <
-    // 2^23), z by a 24-bit multiply-add, 32 bits from a.prim: 2 fma + add + 2
-    // cvt + mad24 + add instead of 3 cvt + 2 mul24 + add3 + a 64-bit add
-    const float kx4 = a.kx4 - (float)(4 * ip0), ky = a.ky - (float)ip1;
+    // 2^23), z by a 24-bit multiply-add, 32 bits from a.prim, all without
+    // float -> int converts: the x/y sum is biased by 2^23 (its bit pattern is
+    // 0x4B000000 + the sum) and z by 2^23 + 2^22 (|z| < 2^21: the low 24 bits
+    // of the pattern are 2^22 + z); kz takes both constants back, mod 2^32
+    const float kx4 = a.kx4 - (float)(4 * ip0) + 8388608.0f, ky = a.ky - (float)ip1;
     const float fXp4 = (float)(4 * a.Xp);
-    const int XpYp4 = (int)(4u * a.XpYp);
-    const unsigned kz = a.kz - (unsigned)XpYp4 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 2);
+    const unsigned XpYp4 = 4u * a.XpYp;
+    const unsigned kz = a.kz - XpYp4 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 2) - 0x4B000000u -
+                        (XpYp4 << 22);
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         if (F32IDX) {
             const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
-            const unsigned off = (unsigned)(int)xy + ((unsigned)__mul24(XpYp4, (int)z) + kz);
+            const unsigned off = __umul24(__float_as_uint(z + 12582912.0f), XpYp4) + __float_as_uint(xy) + kz;
             return ld_off(a.prim, off);
         }
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
@@ -876,14 +896,15 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
         if (EXT != 2) {                // the reference's hard shadow: one sun ray
             cnt.shadow_rays++;
-            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
+            const bool lit = march_sun<VX_RSTEP != 0>(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
                                        cnt.march_witers, reinterpret_cast<const float4 *>(unorm + 256));
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
         } else {                       // ext soft shadows (EXT == 2): lit fraction of the sun samples
             int lit = 0;
             for (int k = 0; k < F.n_sun; k++) {
                 cnt.shadow_rays++;
-                lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch, cnt.march_witers) ? 1 : 0;
+                lit += march_sun<false>(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
+                                        cnt.march_witers) ? 1 : 0;
             }
             shadeFactor = shadeFactor * ((float)lit / (float)F.n_sun);
         }
@@ -1147,7 +1168,6 @@ __device__ void shade_2d(const KernelArgs &a, float d0, float d1, float d2, floa
 #ifndef VX_STAGE
 #define VX_STAGE 1
 #endif
-constexpr int kWG = 256;
 constexpr int kBX = VX_BX;                 // block width in pixels (16 or 32)
 constexpr int kBY = kWG / kBX;             // block height
 constexpr int kBXS = kBX == 32 ? 5 : 4;    // log2(kBX)
