@@ -203,6 +203,20 @@ __device__ __forceinline__ T ld_off(const T *base, unsigned byte_off) {
     return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + byte_off);
 }
 
+// The march's texel load as an asm statement: its result is a plain 32-bit
+// value (the compiler keeps an i8 load's result in 16 bits across the loop's
+// back edge and sign-extends it again every step).  The compiler does not
+// track this load, so wait_vmem(v) must come before any use of v: an
+// s_waitcnt tied to v, placed where the compiler would have put its own.
+// f0..f2 pass through the statement untouched: what reads them (the next
+// step's length) is scheduled after the load, under its latency.
+__device__ __forceinline__ int ld_sbyte_async(const int8_t *base, unsigned byte_off, float &f0, float &f1, float &f2) {
+    int v;
+    asm volatile("global_load_sbyte %0, %4, %5" : "=&v"(v), "+v"(f0), "+v"(f1), "+v"(f2) : "v"(byte_off), "s"(base));
+    return v;
+}
+__device__ __forceinline__ void wait_vmem(int &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
+
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
 __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
     return (unsigned)x + __umul24((unsigned)a.X, (unsigned)y) + __umul24(a.XY, (unsigned)z);
@@ -331,7 +345,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     const unsigned sxpyp = a.SXpYp;
     int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
     // one step of :94-128 -> the texel (-1: left the grid)
-#define VX_PAD_STEP(T)                                                                        \
+#define VX_PAD_STEP(T, ASYNC)                                                                 \
     {                                                                                         \
         float m0, m1, m2;                                                                     \
         if (TAB) {                                                                            \
@@ -349,23 +363,25 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2; /* :120 */                               \
         const unsigned off = __umul24(__float_as_uint(e2), sxpyp) +                           \
                              __float_as_uint(__builtin_fmaf(e1, xpf, e0));                    \
-        T = ld_off(sunb, off); /* :123-128 */                                                 \
-        fetches += T >= 0 ? 1u : 0u;                                                          \
+        T = ASYNC ? ld_sbyte_async(sunb, off, f0, f1, f2) /* :123-128, wait_vmem before use */ \
+                  : (int)ld_off(sunb, off);                                                   \
     }
     int step = 0;                                                                // wave-uniform
     if (maxs > 1) {
         do {
             int t;
-            VX_PAD_STEP(t)
-            len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));                                      // next step, under the load
+            VX_PAD_STEP(t, true)
+            len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));   // next step, under the load
+            wait_vmem(t);
+            fetches += t >= 0 ? 1u : 0u;
             tv = t;
             witers += once_per_wave(1u);         // counted in the loop: step stays a scalar
         } while (tv > 0 && ++step < maxs - 1);
     }
     if (tv > 0) {                              // the MAX_STEPS-th step: only its fetch (stats) matters
-        int t;
-        VX_PAD_STEP(t)
-        (void)t;
+        int t;                                 // (a plain load: dropped unless counted)
+        VX_PAD_STEP(t, false)
+        fetches += t >= 0 ? 1u : 0u;
     }
 #undef VX_PAD_STEP
     return tv != 0;
