@@ -44,6 +44,18 @@
 #ifndef VX_AO_DELTA
 #define VX_AO_DELTA 1
 #endif
+#ifndef VX_SUN_BRICK
+#define VX_SUN_BRICK 0
+#endif
+#if VX_SUN_BRICK
+#define VX_BRICK_CY cy
+#define VX_BRICK_CZ cz
+#define VX_BRICK_UNBIAS unbias
+#else
+#define VX_BRICK_CY 0u
+#define VX_BRICK_CZ 0u
+#define VX_BRICK_UNBIAS 0u
+#endif
 #ifndef VX_PAD_MARCH
 #define VX_PAD_MARCH 0
 #endif
@@ -339,8 +351,21 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     // read from the channel base moved down by 0x4B000000 (vx_scene_create
     // checks Xp*Yp < 2^23 and the sum < 2^32).
     constexpr float kBias = 8388608.0f;
+#if VX_SUN_BRICK
+    // Bricked sunp (VX_SUN_BRICK): 8x4x4 cells per 128-B line, bricks x fastest.
+    // Cells carried as 2^23 + x, 2^23 + 8y, 2^23 + 32z; with X, Y8, Z32 their
+    // patterns' low 24 bits the offset is
+    //   X + 15 (X & ~7) + Y8 + (4 NBX - 1)(Y8 & ~31) + Z32 + (NBXY - 1)(Z32 & ~127)
+    //   = 128 brick + 32 (z & 3) + 8 (y & 3) + (x & 7)   (+ 3 * 0x4B000000)
+    float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(8 * (c1 + a.SB)) + kBias;
+    float e2 = (float)(32 * (c2 + a.SB)) + kBias;
+    const int8_t *sunb = sun;
+    const unsigned unbias = 0u - 3u * 0x4B000000u;   // the three patterns' exponent bits, mod 2^32
+    const unsigned cy = (unsigned)a.SXp, cz = a.SXpYp;
+#else
     float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB) + kBias;
     const int8_t *sunb = sun - 0x4B000000;   // (pointer arithmetic: keeps the global address space)
+#endif
     float len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));
     const unsigned sxpyp = a.SXpYp;
     int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
@@ -359,10 +384,20 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
         f1 = f1 + m1 * len;                                                                   \
         f2 = f2 + m2 * len;                                                                   \
         const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);                     \
-        e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                                   \
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2; /* :120 */                               \
-        const unsigned off = __umul24(__float_as_uint(e2), sxpyp) +                           \
-                             __float_as_uint(__builtin_fmaf(e1, xpf, e0));                    \
+        unsigned off;                                                                         \
+        if (VX_SUN_BRICK) {                                                                   \
+            e0 += fl0; /* :119 (exact), y and z scaled */                                     \
+            e1 = __builtin_fmaf(fl1, 8.0f, e1);                                               \
+            e2 = __builtin_fmaf(fl2, 32.0f, e2);                                              \
+            const unsigned bx = __float_as_uint(e0), by = __float_as_uint(e1);               \
+            const unsigned bz = __float_as_uint(e2);                                          \
+            off = __umul24(bx & ~7u, 15u) + bx + __umul24(by & ~31u, VX_BRICK_CY) + by +      \
+                  __umul24(bz & ~127u, VX_BRICK_CZ) + bz + VX_BRICK_UNBIAS;                   \
+        } else {                                                                              \
+            e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                               \
+            off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(__builtin_fmaf(e1, xpf, e0)); \
+        }                                                                                     \
         T = ASYNC ? ld_sbyte_async(sunb, off, f0, f1, f2) /* :123-128, wait_vmem before use */ \
                   : (int)ld_off(sunb, off);                                                   \
     }
@@ -1585,8 +1620,17 @@ __global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+#if VX_SUN_BRICK
+    // 8x4x4 bricks, one 128-B line each (march_pad); padded extents rounded to whole bricks
+    const size_t Xp = ((size_t)X + 2 * SB + 7) & ~(size_t)7, Yp = ((size_t)Y + 2 * SB + 3) & ~(size_t)3;
+    const size_t Zp = ((size_t)Z + 2 * SB + 3) & ~(size_t)3;
+    const size_t px = (size_t)(x + SB), py = (size_t)(y + SB), pz = (size_t)(z + SB);
+    const size_t j = ((((pz >> 2) * (Yp >> 2) + (py >> 2)) * (Xp >> 3) + (px >> 3)) << 7) | ((pz & 3) << 5) |
+                     ((py & 3) << 3) | (px & 7);
+#else
     const size_t Xp = (size_t)X + 2 * SB, Yp = (size_t)Y + 2 * SB, Zp = (size_t)Z + 2 * SB;
     const size_t j = (size_t)(x + SB) + Xp * ((size_t)(y + SB) + Yp * (size_t)(z + SB));
+#endif
     const uint32_t t = src[i];
     sunp[j] = (int8_t)(t & 0xffu);
     sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);
