@@ -286,6 +286,42 @@ __device__ __forceinline__ float march_len_sg(const SunRay &S, float f0, float f
     return len;
 }
 
+// march_len_sg inside the march loop, where every f_i is a step's
+// f - floor(f), so f_i in [0, 1]: each fract term is one v_fract_f32 (a
+// 4-cycle op, against floor/ceil + subtract = 6).  v_fract(x) is x - floor(x)
+// clamped below 1.0; the two uses never reach the clamp:
+//   s < 0: v_fract(f) = f for f in [0, 1), 0 for f = 1 -- exactly f - floor(f);
+//   s > 0: v_fract(-f) = RN(1 - f) for f in (0, 1], 0 for f = 0 -- exactly
+//          ceil(f) - f, unless RN(1 - f) = 1.0, i.e. 0 < f <= 2^-25.  That f
+//          never occurs after a step taken from an f >= 0 (every step after
+//          the first): the axis moves by RN(RN(r*safe)*len) >= 2^-10 * 1e-4
+//          (|r_i| >= 2^-10 on the fast path, safe >= 1, len >= 1e-4 since
+//          every d >= 1e-4 and |r| <= 1), so f_u >= 9.7e-8 and its fraction
+//          is f_u itself or a multiple of ulp(1) = 2^-23.
+// The first step starts from the surface's fract, which can be slightly
+// negative (the hit point's rounding), so march_pad keeps march_len_sg there.
+#ifndef VX_FRACT
+#define VX_FRACT 1
+#endif
+#ifndef VX_EXY
+#define VX_EXY 1
+#endif
+template <int SG>
+__device__ __forceinline__ float march_len_fract(const SunRay &S, float f0, float f1, float f2) {
+    const float d0 = __builtin_amdgcn_fractf((SG & 1) ? -f0 : f0) + 1e-4f;
+    const float d1 = __builtin_amdgcn_fractf((SG & 2) ? -f1 : f1) + 1e-4f;
+    const float d2 = __builtin_amdgcn_fractf((SG & 4) ? -f2 : f2) + 1e-4f;
+    const float t0 = div_const(d0, S.abs[0], S.rcp[0]);                                // :97
+    const float t1 = div_const(d1, S.abs[1], S.rcp[1]);
+    const float t2 = div_const(d2, S.abs[2], S.rcp[2]);
+    float len = __builtin_fminf(__builtin_fminf(t0, t1), t2);                         // :100-105, one axis
+    if (__builtin_amdgcn_fmed3f(t0, t1, t2) == len) {                                  // ties: literal length
+        const float v0 = t0 == len ? t0 : 0.0f, v1 = t1 == len ? t1 : 0.0f, v2 = t2 == len ? t2 : 0.0f;
+        len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    }
+    return len;
+}
+
 __device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
                            float f1, float f2, unsigned &fetches, unsigned &witers) {
     const FrameConsts &F = a.fc;
@@ -366,6 +402,10 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB) + kBias;
     const int8_t *sunb = sun - 0x4B000000;   // (pointer arithmetic: keeps the global address space)
 #endif
+    // VX_EXY: the x + Xp*y part carried as one biased fp32 integer exy (exact:
+    // 2^23 <= exy < 2^24) and moved by fma(fl1, Xp, fl0) per step -- one add
+    // fewer than moving e0 and e1 and recombining them.
+    float exy = __builtin_fmaf(e1, xpf, e0);
     float len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));
     const unsigned sxpyp = a.SXpYp;
     int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
@@ -394,6 +434,9 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
             const unsigned bz = __float_as_uint(e2);                                          \
             off = __umul24(bx & ~7u, 15u) + bx + __umul24(by & ~31u, VX_BRICK_CY) + by +      \
                   __umul24(bz & ~127u, VX_BRICK_CZ) + bz + VX_BRICK_UNBIAS;                   \
+        } else if (VX_EXY) {                                                                  \
+            exy += __builtin_fmaf(fl1, xpf, fl0); e2 += fl2; /* :119 (exact) */               \
+            off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy);                \
         } else {                                                                              \
             e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                               \
             off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(__builtin_fmaf(e1, xpf, e0)); \
@@ -402,11 +445,24 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
                   : (int)ld_off(sunb, off);                                                   \
     }
     int step = 0;                                                                // wave-uniform
-    if (maxs > 1) {
+    constexpr bool kFract = VX_FRACT && SG >= 0;
+    if (kFract && maxs > 1) {                  // the first step, peeled: its len from march_len_sg
+        int t;
+        VX_PAD_STEP(t, true)
+        len = march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2);
+        wait_vmem(t);
+        fetches += t >= 0 ? 1u : 0u;
+        tv = t;
+        witers += once_per_wave(1u);
+        ++step;
+    }
+    if (maxs > 1 && tv > 0 && step < maxs - 1) {
         do {
             int t;
             VX_PAD_STEP(t, true)
-            len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));   // next step, under the load
+            len = (SG < 0 ? march_len(S, f0, f1, f2)
+                          : (kFract ? march_len_fract<(SG < 0 ? 0 : SG)>(S, f0, f1, f2)
+                                    : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2)));   // next step, under the load
             wait_vmem(t);
             fetches += t >= 0 ? 1u : 0u;
             tv = t;
@@ -896,10 +952,35 @@ constexpr float kRoughAmp = 0.1f;
 // EXT: the extension instantiation (rough normals, soft shadows); has_ray:
 // rayDir is given (a surface seen in a reflection) instead of the camera ray
 // to the fragment (:154).  ray_out receives the rayDir used.
+// The sun-facing factor of render.frag:228-229 with the (ext ROUGH) shading
+// normal, exactly as shade_block computes it: the soft-shadow pass of k_render
+// asks it first, to know which fragments march.
+template <int EXT>
+__device__ float block_shade_factor(const KernelArgs &a, const float *unorm, const Surf &g) {
+    const FrameConsts &F = a.fc;
+    const int ni = g.nidx;
+    if (!(EXT && (F.flags & VX_FLAG_ROUGH))) return F.shadeFactor[ni];
+    const float n0 = ni == 0 ? 1.0f : (ni == 1 ? -1.0f : 0.0f);
+    const float n1 = ni == 2 ? 1.0f : (ni == 3 ? -1.0f : 0.0f);
+    const float n2 = ni == 4 ? 1.0f : (ni == 5 ? -1.0f : 0.0f);
+    const int ax = ni >> 1;
+    const float u = ax == 0 ? (float)g.c1 + g.f1 : (float)g.c0 + g.f0;
+    const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;
+    float w0, w1, w2, m0, m1, m2;
+    white(a, unorm, u * kRoughScale, v * kRoughScale, w0, w1, w2);
+    if (VX_ROUGH_RCP)
+        normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+    else
+        normalize3(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+    return F.sun[2] < 0.0f ? 0.0f : sqrtf(gmax(0.0f, (m0 * F.sun[0] + m1 * F.sun[1]) + m2 * F.sun[2]));
+}
+
+// lit_given >= 0 (EXT 2): the soft-shadow samples of this fragment were
+// marched by k_render's wave pass, lit_given of them lit.
 template <int EXT>
 __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt,
                             bool has_ray = false, float q0 = 0.0f, float q1 = 0.0f, float q2 = 0.0f,
-                            float *ray_out = nullptr) {
+                            float *ray_out = nullptr, int lit_given = -1) {
     const FrameConsts &F = a.fc;
     const int ni = g.nidx;
     const float n0 = ni == 0 ? 1.0f : (ni == 1 ? -1.0f : 0.0f);
@@ -950,6 +1031,8 @@ __device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf 
             const bool lit = march_sun<VX_RSTEP != 0>(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
                                        cnt.march_witers, reinterpret_cast<const float4 *>(unorm + 256));
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
+        } else if (lit_given >= 0) {   // marched by the wave pass (k_render)
+            shadeFactor = shadeFactor * ((float)lit_given / (float)F.n_sun);
         } else {                       // ext soft shadows (EXT == 2): lit fraction of the sun samples
             int lit = 0;
             for (int k = 0; k < F.n_sun; k++) {
@@ -1216,6 +1299,9 @@ __device__ void shade_2d(const KernelArgs &a, float d0, float d1, float d2, floa
 #ifndef VX_BX
 #define VX_BX 32
 #endif
+#ifndef VX_SOFT_TAB
+#define VX_SOFT_TAB 0
+#endif
 #ifndef VX_STAGE
 #define VX_STAGE 1
 #endif
@@ -1237,6 +1323,7 @@ void k_render(KernelArgs a) {
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     __shared__ float4 s_lds[64 + 128];
     __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
+    __shared__ float4 s_rk[EXT == 2 && VX_SOFT_TAB ? 4 * 128 : 1];   // EXT 2: per wave, r*k of the current sample
     float *s_unorm = reinterpret_cast<float *>(s_lds);
 #pragma unroll
     for (int i = threadIdx.x; i < 256; i += kWG)        // = (float)i / 255.0f, the IEEE quotient (§5)
@@ -1279,6 +1366,36 @@ void k_render(KernelArgs a) {
         const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
         Surf g[2];
         const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt);
+        // EXT 2 (soft shadows): the samples of the first surface marched here,
+        // one sample at a time for the whole wave, each with an LDS table of its
+        // r*safe products built by all 64 lanes (the march_pad TAB form of the
+        // hard shadow).  Later surfaces (behind glass, in a reflection) march
+        // in shade_block.
+        int lit0 = -1;
+        if (EXT == 2 && VX_SOFT_TAB) {
+            const bool need = n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
+                              block_shade_factor<EXT>(a, s_unorm, g[0]) > 0.0f;
+            if (__ballot(need)) {
+                lit0 = 0;
+                float4 *tab = s_rk + (threadIdx.x & ~63) * 2;
+                for (int k = 0; k < F.n_sun; k++) {
+                    const SunRay S = F.sun_k[k];
+                    const float k0 = (float)lane, k1 = (float)(lane + 64);
+                    tab[lane] = make_float4(S.r[0] * k0, S.r[1] * k0, S.r[2] * k0, 0.0f);
+                    tab[lane + 64] = make_float4(S.r[0] * k1, S.r[1] * k1, S.r[2] * k1, 0.0f);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    if (need) {
+                        cnt.shadow_rays++;
+                        lit0 += march_sun<true>(a, S, g[0].c0, g[0].c1, g[0].c2, g[0].f0, g[0].f1, g[0].f2,
+                                                cnt.shadow_fetch, cnt.march_witers, tab) ? 1 : 0;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (!need) lit0 = -1;
+            }
+        }
         float rgba[4];
         if (F.flags & VX_FLAG_PRIMARY_ONLY) {
             primary_only_colour(n, g[0], rgba);
@@ -1290,7 +1407,7 @@ void k_render(KernelArgs a) {
             shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
             float rd[3];
-            shade_block<EXT>(a, s_unorm, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd);
+            shade_block<EXT>(a, s_unorm, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
             if (g[0].id == 2) {
                 n_glass = 1;
                 if (EXT && (F.flags & VX_FLAG_REFLECT)) {
