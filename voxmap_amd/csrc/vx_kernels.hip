@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "vx_internal.h"
 
 // Diagnostic padding (A/B only, never in the product build): VX_PAD_MARCH /
@@ -228,6 +230,38 @@ __device__ __forceinline__ int ld_sbyte_async(const int8_t *base, unsigned byte_
     return v;
 }
 __device__ __forceinline__ void wait_vmem(int &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
+__device__ __forceinline__ void wait_vmem(float &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
+
+// VX_FMT_LOAD: the march texel through a typed buffer load whose descriptor
+// says "8-bit, SSCALED" (DATA_FORMAT 1, NUM_FORMAT 3, DST_SEL_X = X): the
+// texture data unit returns (float)(int8)texel, so the loop needs no
+// byte -> float convert.  The descriptor's base is the channel moved down by
+// the offset bias (0x4B000000, march_pad), num_records = 2^32 - 1 (offsets are
+// in bounds by the -1 border, as for the global load).
+#ifndef VX_FMT_LOAD
+#define VX_FMT_LOAD 1
+#endif
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 fmt_rsrc(const int8_t *base) {
+    const unsigned long long p = (unsigned long long)base;
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((unsigned)p);
+    r.y = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32) & 0xffffu);
+    r.z = 0xffffffffu;
+    r.w = 0x0000B004u;
+    return r;
+}
+__device__ __forceinline__ float ld_fmt_async(u32x4 rsrc, unsigned byte_off, float &f0, float &f1, float &f2) {
+    float v;
+    asm volatile("buffer_load_format_x %0, %4, %5, 0 offen" : "=&v"(v), "+v"(f0), "+v"(f1), "+v"(f2)
+                 : "v"(byte_off), "s"(rsrc));
+    return v;
+}
+__device__ __forceinline__ float ld_fmt(u32x4 rsrc, unsigned byte_off) {
+    float v;
+    asm("buffer_load_format_x %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(byte_off), "s"(rsrc));
+    return v;
+}
 
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
 __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
@@ -408,16 +442,20 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     float exy = __builtin_fmaf(e1, xpf, e0);
     float len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));
     const unsigned sxpyp = a.SXpYp;
-    int tv = 1;                                // texel of the current cell = safe (render.frag:86: 1)
+    // kFmt: the texel arrives as a float (VX_FMT_LOAD, soft-shadow samples)
+    constexpr bool kFmt = VX_FMT_LOAD && !TAB && !VX_SUN_BRICK;
+    typedef typename std::conditional<kFmt, float, int>::type texel_t;
+    const u32x4 rsrc = fmt_rsrc(sunb);
+    texel_t tv = 1;                            // texel of the current cell = safe (render.frag:86: 1)
     // one step of :94-128 -> the texel (-1: left the grid)
 #define VX_PAD_STEP(T, ASYNC)                                                                 \
     {                                                                                         \
         float m0, m1, m2;                                                                     \
-        if (TAB) {                                                                            \
-            const float4 q = rstep[tv];                                                       \
+        if constexpr (TAB) {                                                                  \
+            const float4 q = rstep[(int)tv];                                                  \
             m0 = q.x; m1 = q.y; m2 = q.z;                                                     \
         } else {                                                                              \
-            const float safe = cvt_f32_ubyte0((uint32_t)tv); /* 1..126 in the loop */          \
+            const float safe = kFmt ? (float)tv : cvt_f32_ubyte0((uint32_t)tv); /* 1..126 */  \
             m0 = r0 * safe; m1 = r1 * safe; m2 = r2 * safe;                                   \
         }                                                                                     \
         f0 = f0 + m0 * len; /* :118 */                                                        \
@@ -441,13 +479,16 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
             e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                               \
             off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(__builtin_fmaf(e1, xpf, e0)); \
         }                                                                                     \
-        T = ASYNC ? ld_sbyte_async(sunb, off, f0, f1, f2) /* :123-128, wait_vmem before use */ \
-                  : (int)ld_off(sunb, off);                                                   \
+        if constexpr (kFmt)                                                                   \
+            T = ASYNC ? ld_fmt_async(rsrc, off, f0, f1, f2) : ld_fmt(rsrc, off);             \
+        else                                                                                  \
+            T = ASYNC ? ld_sbyte_async(sunb, off, f0, f1, f2) /* :123-128, wait_vmem before use */ \
+                      : (int)ld_off(sunb, off);                                               \
     }
     int step = 0;                                                                // wave-uniform
     constexpr bool kFract = VX_FRACT && SG >= 0;
     if (kFract && maxs > 1) {                  // the first step, peeled: its len from march_len_sg
-        int t;
+        texel_t t;
         VX_PAD_STEP(t, true)
         len = march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2);
         wait_vmem(t);
@@ -458,7 +499,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     }
     if (maxs > 1 && tv > 0 && step < maxs - 1) {
         do {
-            int t;
+            texel_t t;
             VX_PAD_STEP(t, true)
             len = (SG < 0 ? march_len(S, f0, f1, f2)
                           : (kFract ? march_len_fract<(SG < 0 ? 0 : SG)>(S, f0, f1, f2)
@@ -470,7 +511,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
         } while (tv > 0 && ++step < maxs - 1);
     }
     if (tv > 0) {                              // the MAX_STEPS-th step: only its fetch (stats) matters
-        int t;                                 // (a plain load: dropped unless counted)
+        texel_t t;                             // (a plain load: dropped unless counted)
         VX_PAD_STEP(t, false)
         fetches += t >= 0 ? 1u : 0u;
     }
