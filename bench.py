@@ -205,7 +205,7 @@ def main():
                                  sun_radius=args.sun_radius if samples > 1 else 0.0)
     K = max(1, args.inflight)
 
-    gather_desc = mg = None
+    gather_desc = mg = split_ms = None
     if world == 1:
         r = single_gpu(torch, vx, scene, frame, W, H, K, args.steps, args.warmup, args.settle_ms)
         stats, wall, settle_steps, ev_ms = r["stats"], r["wall_s"], r["settle"], r["ev_ms"]
@@ -276,6 +276,32 @@ def main():
             tt = tt.cuda()
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall = float(tt.item())
+        if mg is not None:
+            # render and gather timed apart (one stream, one frame at a
+            # time, max over ranks): vx_render_bands of this rank's bands, then
+            # vx_mgpu_gather alone (collective)
+            try:
+                mine = vx.mgpu_bands(H, BAND, world, rank)
+                s0 = streams[0].cuda_stream
+
+                def r_only():
+                    if mine:
+                        scene.render_bands(frame, BAND, mine, frames[0].data_ptr(), inplace=True, stream=s0)
+
+                def g_only():
+                    mg.gather(W, H, BAND, frames[0].data_ptr(), stream=s0)
+                tr, _ = timed(torch, r_only, args.steps, 2, 0.0, dist)
+                tg, _ = timed(torch, g_only, args.steps, 2, 0.0, dist)
+                t2 = torch.tensor([tr, tg], dtype=torch.float64)
+                dist.all_reduce(t2, op=dist.ReduceOp.MAX)
+                split_ms = {"render_ms": round(1000.0 * float(t2[0]) / args.steps, 4),
+                            "gather_ms": round(1000.0 * float(t2[1]) / args.steps, 4),
+                            "gather_bytes": int(W * 4 * sum(min(BAND, H - b * BAND)
+                                                            for b in range(-(-H // BAND)) if b % world)),
+                            "how": "one stream, one frame at a time, max over ranks (the timed step overlaps "
+                                   "frames in flight, so it is less than the sum)"}
+            except Exception as e:            # never let the diagnostic break the bench line
+                split_ms = {"error": str(e)}
     ms_per_step = 1000.0 * wall / args.steps
 
     v1 = c5 = None
@@ -354,7 +380,8 @@ def main():
                 "clock_settle": {"ms": args.settle_ms, "untimed_frames": settle_steps},
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
                 "shards": ({"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
-                            "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc}
+                            "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc,
+                            "split_ms": split_ms}
                            if world > 1 else None),
                 "fps": round(1000.0 / ms_per_step, 2),
                 "inflight": {"frames": K, "streams": K, "framebuffers": K,

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 4
+#define VX_ABI_VERSION 5
 
 /* error codes */
 #define VX_OK 0
@@ -210,6 +210,11 @@ int vx_mgpu_unique_id(void *uid_out);
 int vx_mgpu_create(vx_scene *scene, const void *uid, int nranks, int rank, vx_mgpu **out);
 int vx_mgpu_render(vx_mgpu *m, const vx_frame_params *p, int w, int h, int band_rows, int pixel_format,
                    void *frame_device, void *stream, vx_stats *stats);
+/* The gather step of vx_mgpu_render alone (collective, stream-ordered): the
+ * bands of ranks 1..n-1 from their frame rows into rank 0's.  vx_mgpu_render
+ * = vx_render_bands of this rank's bands (in place) + vx_mgpu_gather; the bench
+ * times the two apart (gather and render time reported separately). */
+int vx_mgpu_gather(vx_mgpu *m, int w, int h, int band_rows, int pixel_format, void *frame_device, void *stream);
 int vx_mgpu_rank(const vx_mgpu *m, int *nranks, int *rank);
 void vx_mgpu_destroy(vx_mgpu *m);
 /* The deal: the band ids of `rank` (ascending) into ids[0..cap); returns their count. */

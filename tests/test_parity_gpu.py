@@ -455,7 +455,10 @@ def test_mgpu_single_rank_equals_full_frame(full_scene):
     try:
         frame = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda:0")
         st = mg.render(fr, 64, frame.data_ptr(), stats=True)
+        mg.gather(w, h, 64, frame.data_ptr())        # the gather step alone (bench's split timing)
         torch.cuda.synchronize()
+        with pytest.raises(RuntimeError):
+            mg.gather(w, h, 60, frame.data_ptr())    # band rows must be a multiple of 8
     finally:
         mg.close()
     assert np.array_equal(frame.cpu().numpy(), full)

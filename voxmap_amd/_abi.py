@@ -28,7 +28,7 @@ FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
 FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
 FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary index path
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 4
+ABI_VERSION = 5
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128
 
@@ -97,6 +97,7 @@ SIGNATURES = [
     ("vx_mgpu_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("vx_mgpu_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_void_p, C.c_void_p, C.POINTER(Stats)]),
+    ("vx_mgpu_gather", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     ("vx_mgpu_rank", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("vx_mgpu_destroy", None, [C.c_void_p]),
     ("vx_mgpu_bands", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int]),

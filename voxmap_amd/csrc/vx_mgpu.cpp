@@ -106,7 +106,6 @@ int vx_mgpu_render(vx_mgpu *m, const vx_frame_params *p, int w, int h, int band_
         m->band_rows = band_rows;
     }
     if (hipSetDevice(m->device) != hipSuccess) return set_error(VX_EDEVICE, "vx_mgpu_render: hipSetDevice failed");
-    hipStream_t st = (hipStream_t)stream;
     if (!m->mine.empty()) {
         const int rc = vx_render_bands(m->scene, p, w, h, band_rows, m->mine.data(), (int)m->mine.size(),
                                        pixel_format, frame_device, 1, stream, stats);
@@ -114,7 +113,19 @@ int vx_mgpu_render(vx_mgpu *m, const vx_frame_params *p, int w, int h, int band_
     } else if (stats) {
         std::memset(stats, 0, sizeof *stats);
     }
+    return vx_mgpu_gather(m, w, h, band_rows, pixel_format, frame_device, stream);
+}
+
+int vx_mgpu_gather(vx_mgpu *m, int w, int h, int band_rows, int pixel_format, void *frame_device, void *stream) {
+    if (!m || !frame_device) return set_error(VX_EINVAL, "vx_mgpu_gather: null argument");
+    if (band_rows <= 0 || band_rows % VX_TILE_ALIGN_Y)
+        return set_error(VX_EINVAL, "vx_mgpu_gather: band_rows must be a positive multiple of 8");
+    if (h <= 0 || w <= 0) return set_error(VX_EINVAL, "vx_mgpu_gather: frame size out of range");
+    if (pixel_format != VX_PIXEL_RGBA8 && pixel_format != VX_PIXEL_RGBA32F)
+        return set_error(VX_EINVAL, "vx_mgpu_gather: unknown pixel format");
     if (m->nranks == 1) return VX_OK;
+    if (hipSetDevice(m->device) != hipSuccess) return set_error(VX_EDEVICE, "vx_mgpu_gather: hipSetDevice failed");
+    hipStream_t st = (hipStream_t)stream;
     // the gather: every band not rank 0's goes from its owner's frame rows to rank 0's
     const size_t px = pixel_format == VX_PIXEL_RGBA32F ? 16 : 4;
     const size_t row_bytes = (size_t)w * px;

@@ -274,6 +274,12 @@ class MultiGPU:
                                    C.byref(st) if st is not None else None))
         return st
 
+    def gather(self, width: int, height: int, band_rows: int, frame_ptr: int, *, pixel_format=_abi.PIXEL_RGBA8,
+               stream=None):
+        """The gather step of render() alone (collective): ranks 1..n-1's bands into rank 0's frame rows."""
+        check(lib().vx_mgpu_gather(self._h, int(width), int(height), int(band_rows), pixel_format,
+                                   C.c_void_p(frame_ptr), C.c_void_p(stream) if stream else None))
+
     def close(self):
         if getattr(self, "_h", None) is not None:
             lib().vx_mgpu_destroy(self._h)
