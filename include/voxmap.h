@@ -79,6 +79,11 @@ extern "C" {
 /* Diagnostics: force the integer primary-index path (the fp32 one is chosen
  * whenever it is exact; both give identical frames). */
 #define VX_FLAG_INT_INDEX 0x40u
+/* Soft shadows (shadow_samples > 1) marched by the pooled wave pass: the
+ * marching fragments are compacted by a ballot and their samples dealt over
+ * all 64 lanes (DESIGN.md §6 "C5").  Identical frames; off by default because
+ * it measures slower on C5. */
+#define VX_FLAG_SOFT_POOL 0x80u
 #define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;

@@ -254,6 +254,11 @@ EXT_CASES = {
     "soft_sun_low": dict(shadow_samples=6, sun_radius=0.3, sun=(0.9, 0.3, 0.05)),   # samples below the horizon
     "soft_axis_zero": dict(shadow_samples=4, sun_radius=0.0, sun=(0.6, 0.0, 0.8)),  # literal march per sample
     "full_no_ao_no_clouds": dict(flags=0x30 | 0x2 | 0x4),
+    # VX_FLAG_SOFT_POOL (0x80): the same samples marched by the pooled wave pass
+    "soft8_pool": dict(flags=0x80, shadow_samples=8, sun_radius=0.05),
+    "soft6_pool": dict(flags=0x80, shadow_samples=6, sun_radius=0.05),            # 8-lane groups, 2 idle lanes
+    "soft16_full_pool": dict(flags=0x30 | 0x80, shadow_samples=16, sun_radius=0.04),
+    "soft_sun_low_pool": dict(flags=0x80, shadow_samples=6, sun_radius=0.3, sun=(0.9, 0.3, 0.05)),  # mixed: falls back
 }
 
 
@@ -359,6 +364,32 @@ def test_c5_rows_soft_shadows_full_quality(noise):
     rows = np.arange(step // 2, c["h"], step)
     _compare(img, ref, rows)
     assert st.primary_cap_hits == 0
+
+
+def test_soft_pool_equals_per_sample_march(noise):
+    """VX_FLAG_SOFT_POOL at C5 (3^3 field, 16 samples, full quality): the pooled
+    wave march gives the same RGBA8 frame and the same work counters as the
+    per-sample loop, on the whole 3840x2160 frame."""
+    import torch
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid("s_up3")
+    Z, Y, X = grid.shape
+    c = presets.CONFIGS["C5"]
+    outs, sts = [], []
+    with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
+        for extra in (0, vx.FLAG_SOFT_POOL):
+            fr = presets.camera_frame("K1", c["w"], c["h"], scale=3.0, flags=vx.FLAG_FULL_QUALITY | extra,
+                                      shadow_samples=16, sun_radius=0.03)
+            out = torch.zeros(c["w"] * c["h"] * 4, dtype=torch.uint8, device="cuda:0")
+            sts.append(sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True))
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    a, b = sts[0].as_dict(), sts[1].as_dict()
+    for k in ("shadow_rays", "shadow_fetches", "primary_fetches", "ao_samples", "alg_bytes"):
+        assert a[k] == b[k], (k, a[k], b[k])
 
 
 # ---- the reference's map.bin air encoding (VERDICT r01 next #2) ------------------

@@ -1,1 +1,2 @@
-TAG=r01 bash tools/profile.sh && timeout -k 10 300 python bench.py > gpurun_out/bench_full.log 2>&1; tail -1 gpurun_out/bench_full.log
+cd "${GRAFT_REPO_ROOT}" && mkdir -p gpurun_out && \
+PYTEST_ARGS="--timeout 120 --timeout-method thread" BENCH_ARGS="--no-cpu" bash tools/gpu_check.sh

@@ -131,6 +131,20 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
     float dirs[VX_MAX_SHADOW_SAMPLES][3];
     sun_samples(p.sun_dir, p.sun_radius, fc.n_sun, dirs);
     for (int k = 0; k < fc.n_sun; k++) sun_ray(dirs[k], fc.sun_k[k]);
+    // the pooled soft-shadow march (vx_kernels.hip) runs one loop specialised on
+    // the axis signs for every sample: only when they all agree
+    fc.soft_sg = -1;
+    fc.soft_lg = 0;
+    while ((1 << fc.soft_lg) < fc.n_sun) fc.soft_lg++;
+    if (fc.n_sun > 1) {
+        auto sg = [](const SunRay &r) {
+            return (r.sign[0] > 0.0f ? 1 : 0) | (r.sign[1] > 0.0f ? 2 : 0) | (r.sign[2] > 0.0f ? 4 : 0);
+        };
+        bool same = true;
+        for (int k = 0; k < fc.n_sun; k++)
+            same = same && fc.sun_k[k].fast && sg(fc.sun_k[k]) == sg(fc.sun_k[0]) && fc.sun_k[k].up == fc.sun_k[0].up;
+        if (same) fc.soft_sg = sg(fc.sun_k[0]);
+    }
 }
 
 }  // namespace vx

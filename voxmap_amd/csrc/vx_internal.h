@@ -48,6 +48,9 @@ struct FrameConsts {
     int quality;
     unsigned flags;
     int n_sun;                         // ext: sun samples per shadow (1 = the reference's hard shadow)
+    int soft_sg;                       // ext: axis-sign pattern shared by every sample (bit i: r_i > 0), all
+                                       // of them on the fast path and reading one channel; -1 otherwise
+    int soft_lg;                       // ext: log2 of the lanes per fragment in the pooled march (2^lg >= n_sun)
     SunRay sun_k[VX_MAX_SHADOW_SAMPLES];   // ext: soft-shadow sample directions
 };
 

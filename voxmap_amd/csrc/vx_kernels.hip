@@ -1343,6 +1343,9 @@ __device__ void shade_2d(const KernelArgs &a, float d0, float d1, float d2, floa
 #ifndef VX_SOFT_TAB
 #define VX_SOFT_TAB 0
 #endif
+#ifndef VX_POOL
+#define VX_POOL 0
+#endif
 #ifndef VX_STAGE
 #define VX_STAGE 1
 #endif
@@ -1359,12 +1362,33 @@ static_assert(kBX == 16 || kBX == 32, "VX_BX must be 16 or 32");
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
 __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
+    // EXT 3 (VX_FLAG_SOFT_POOL): the soft-shadow instantiation (EXT 2) with the
+    // first surface's samples marched by the pooled wave pass
+    constexpr int XE = EXT == 3 ? 2 : EXT;
+    constexpr bool kPoolOn = EXT == 3 || (EXT == 2 && VX_POOL);
     // LDS: [0, 256) unorm8 -> float table, b/255 as IEEE quotients (render.frag:38
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     __shared__ float4 s_lds[64 + 128];
     __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
-    __shared__ float4 s_rk[EXT == 2 && VX_SOFT_TAB ? 4 * 128 : 1];   // EXT 2: per wave, r*k of the current sample
+    __shared__ float4 s_rk[XE == 2 && VX_SOFT_TAB ? 4 * 128 : 1];   // EXT 2: per wave, r*k of the current sample
+    // EXT 2, VX_POOL: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
+    // the compacted marching fragments' start (fract, cell) and lit counts
+    constexpr int kPool = kPoolOn ? 1 : 0;
+    __shared__ float4 s_sunk[kPool ? 3 * VX_MAX_SHADOW_SAMPLES : 1];
+    __shared__ float4 s_pf[kPool ? kWG : 1];
+    __shared__ int4 s_pc[kPool ? kWG : 1];
+    __shared__ int s_plit[kPool ? kWG : 1];
+    if (kPool) {
+        for (int k = 0; k < a.fc.n_sun; k++) {          // uniform k: scalar loads of the kernel argument
+            if (threadIdx.x == k) {
+                const SunRay &Sk = a.fc.sun_k[k];
+                s_sunk[3 * k] = make_float4(Sk.r[0], Sk.r[1], Sk.r[2], 0.0f);
+                s_sunk[3 * k + 1] = make_float4(Sk.abs[0], Sk.abs[1], Sk.abs[2], 0.0f);
+                s_sunk[3 * k + 2] = make_float4(Sk.rcp[0], Sk.rcp[1], Sk.rcp[2], 0.0f);
+            }
+        }
+    }
     float *s_unorm = reinterpret_cast<float *>(s_lds);
 #pragma unroll
     for (int i = threadIdx.x; i < 256; i += kWG)        // = (float)i / 255.0f, the IEEE quotient (§5)
@@ -1413,9 +1437,9 @@ void k_render(KernelArgs a) {
         // hard shadow).  Later surfaces (behind glass, in a reflection) march
         // in shade_block.
         int lit0 = -1;
-        if (EXT == 2 && VX_SOFT_TAB) {
+        if (XE == 2 && VX_SOFT_TAB) {
             const bool need = n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
-                              block_shade_factor<EXT>(a, s_unorm, g[0]) > 0.0f;
+                              block_shade_factor<XE>(a, s_unorm, g[0]) > 0.0f;
             if (__ballot(need)) {
                 lit0 = 0;
                 float4 *tab = s_rk + (threadIdx.x & ~63) * 2;
@@ -1437,6 +1461,60 @@ void k_render(KernelArgs a) {
                 if (!need) lit0 = -1;
             }
         }
+        if (kPoolOn && !VX_SOFT_TAB && F.soft_sg >= 0 && a.sunp) {
+            // Pooled soft shadows (VX_POOL): the fragments of the wave that march
+            // are compacted by a ballot, and each pass deals 64 / G of them with
+            // G = 2^soft_lg lanes per fragment, lane k of a group marching sample
+            // k.  A wave load then touches the few cache lines around 64 / G
+            // surface points instead of one line per pixel, and lanes whose own
+            // pixel does not march (sky, faces turned from the sun) march for
+            // the others.  Same exact march_pad, lit counted per fragment in LDS.
+            const bool need = n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
+                              block_shade_factor<XE>(a, s_unorm, g[0]) > 0.0f;
+            const unsigned long long mask = __ballot(need);
+            if (mask) {
+                const int wb = threadIdx.x & ~63;                // this wave's 64 slots
+                const int nf = __popcll(mask);
+                const int slot = __popcll(mask & ((1ull << lane) - 1ull));
+                if (need) {
+                    s_pf[wb + slot] = make_float4(g[0].f0, g[0].f1, g[0].f2, 0.0f);
+                    s_pc[wb + slot] = make_int4(g[0].c0, g[0].c1, g[0].c2, 0);
+                    s_plit[wb + slot] = 0;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const int lg = F.soft_lg;
+                const int k = lane & ((1 << lg) - 1);
+                const bool klane = k < F.n_sun;
+                SunRay S;                                         // this lane's sample (per-lane values)
+                const float4 q0 = s_sunk[3 * k], q1 = s_sunk[3 * k + 1], q2 = s_sunk[3 * k + 2];
+                S.r[0] = q0.x; S.r[1] = q0.y; S.r[2] = q0.z;
+                S.abs[0] = q1.x; S.abs[1] = q1.y; S.abs[2] = q1.z;
+                S.rcp[0] = q2.x; S.rcp[1] = q2.y; S.rcp[2] = q2.z;
+                const int8_t *ch = F.sun_k[0].up ? a.sunp : a.sunp + a.sunp_texels;
+                for (int base = 0; base < nf; base += 64 >> lg) {     // wave-uniform passes
+                    const int fs = base + (lane >> lg);
+                    if (klane && fs < nf) {
+                        const float4 pf = s_pf[wb + fs];
+                        const int4 pc = s_pc[wb + fs];
+                        cnt.shadow_rays++;
+                        bool lit;
+                        switch (F.soft_sg) {
+#define VX_SGP(K) case K: lit = march_pad<K, false>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
+                                                    cnt.shadow_fetch, cnt.march_witers, nullptr); break;
+                            VX_SGP(0) VX_SGP(1) VX_SGP(2) VX_SGP(3) VX_SGP(4) VX_SGP(5) VX_SGP(6)
+                            default: lit = march_pad<7, false>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
+                                                               cnt.shadow_fetch, cnt.march_witers, nullptr);
+#undef VX_SGP
+                        }
+                        if (lit) atomicAdd(&s_plit[wb + fs], 1);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (need) lit0 = s_plit[wb + slot];
+            }
+        }
         float rgba[4];
         if (F.flags & VX_FLAG_PRIMARY_ONLY) {
             primary_only_colour(n, g[0], rgba);
@@ -1448,13 +1526,13 @@ void k_render(KernelArgs a) {
             shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
         } else {
             float rd[3];
-            shade_block<EXT>(a, s_unorm, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
+            shade_block<XE>(a, s_unorm, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
             if (g[0].id == 2) {
                 n_glass = 1;
-                if (EXT && (F.flags & VX_FLAG_REFLECT)) {
+                if (XE && (F.flags & VX_FLAG_REFLECT)) {
                     // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
                     float refl[3];
-                    reflect_color<EXT>(a, s_unorm, g[0], rd, refl, cnt);
+                    reflect_color<XE>(a, s_unorm, g[0], rd, refl, cnt);
                     const int ax = g[0].nidx >> 1;
                     const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
                     const float x = 1.0f - cs, x2 = x * x;
@@ -1463,7 +1541,7 @@ void k_render(KernelArgs a) {
                     for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
                 }
                 float dst[4];
-                if (n == 2) shade_block<EXT>(a, s_unorm, g[1], dst, cnt);
+                if (n == 2) shade_block<XE>(a, s_unorm, g[1], dst, cnt);
                 else shade_sky(a, s_unorm, d0, d1, d2, dst, cnt);
                 const float al = rgba[3];
 #pragma unroll
@@ -1659,9 +1737,11 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
         if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
         return (int)hipGetLastError();
     }
-    const int ext = a.fc.n_sun > 1 ? 2 : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
+    const int ext = a.fc.n_sun > 1 ? ((a.fc.flags & VX_FLAG_SOFT_POOL) ? 3 : 2)
+                                   : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
 #define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
-#define VX_LE(F, S, T) do { if (ext == 2) VX_L(F, S, T, 2); else if (ext) VX_L(F, S, T, 1); else VX_L(F, S, T, 0); } while (0)
+#define VX_LE(F, S, T) do { if (ext == 3) VX_L(F, S, T, 3); else if (ext == 2) VX_L(F, S, T, 2); \
+                                else if (ext) VX_L(F, S, T, 1); else VX_L(F, S, T, 0); } while (0)
 #define VX_LT(F, S) do { if (tiled) VX_LE(F, S, true); else VX_LE(F, S, false); } while (0)
     if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_LT(0, true); else VX_LT(0, false); }
     else { if (st) VX_LT(1, true); else VX_LT(1, false); }
