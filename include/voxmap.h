@@ -84,6 +84,10 @@ extern "C" {
  * all 64 lanes (DESIGN.md §6 "C5").  Identical frames; off by default because
  * it measures slower on C5. */
 #define VX_FLAG_SOFT_POOL 0x80u
+/* VX_FLAG_SOFT_POOL plus LDS brick staging (the 8x8x8 march-channel block
+ * around each fragment staged per pass; DESIGN.md §6 "C5").  Identical frames;
+ * an experiment, off by default (slower on C5). */
+#define VX_FLAG_SOFT_BRICK 0x100u
 #define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;

@@ -259,6 +259,10 @@ EXT_CASES = {
     "soft6_pool": dict(flags=0x80, shadow_samples=6, sun_radius=0.05),            # 8-lane groups, 2 idle lanes
     "soft16_full_pool": dict(flags=0x30 | 0x80, shadow_samples=16, sun_radius=0.04),
     "soft_sun_low_pool": dict(flags=0x80, shadow_samples=6, sun_radius=0.3, sun=(0.9, 0.3, 0.05)),  # mixed: falls back
+    # VX_FLAG_SOFT_BRICK (0x100): pooled + LDS 8^3 brick staging
+    "soft16_brick": dict(flags=0x100, shadow_samples=16, sun_radius=0.05),
+    "soft12_full_brick": dict(flags=0x30 | 0x100, shadow_samples=12, sun_radius=0.04),
+    "soft16_brick_sun_neg": dict(flags=0x100, shadow_samples=16, sun_radius=0.05, sun=(-0.5, -0.6, 0.62)),
 }
 
 
@@ -367,9 +371,10 @@ def test_c5_rows_soft_shadows_full_quality(noise):
 
 
 def test_soft_pool_equals_per_sample_march(noise):
-    """VX_FLAG_SOFT_POOL at C5 (3^3 field, 16 samples, full quality): the pooled
-    wave march gives the same RGBA8 frame and the same work counters as the
-    per-sample loop, on the whole 3840x2160 frame."""
+    """VX_FLAG_SOFT_POOL and VX_FLAG_SOFT_BRICK at C5 (3^3 field, 16 samples,
+    full quality): the pooled wave march, with and without LDS brick staging,
+    gives the same RGBA8 frame and the same work counters as the per-sample
+    loop, on the whole 3840x2160 frame."""
     import torch
     import voxmap_amd as vx
     from voxmap_amd import presets
@@ -379,17 +384,18 @@ def test_soft_pool_equals_per_sample_march(noise):
     outs, sts = [], []
     with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
                   noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
-        for extra in (0, vx.FLAG_SOFT_POOL):
+        for extra in (0, vx.FLAG_SOFT_POOL, vx.FLAG_SOFT_BRICK):
             fr = presets.camera_frame("K1", c["w"], c["h"], scale=3.0, flags=vx.FLAG_FULL_QUALITY | extra,
                                       shadow_samples=16, sun_radius=0.03)
             out = torch.zeros(c["w"] * c["h"] * 4, dtype=torch.uint8, device="cuda:0")
             sts.append(sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True))
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy())
-    assert np.array_equal(outs[0], outs[1])
-    a, b = sts[0].as_dict(), sts[1].as_dict()
-    for k in ("shadow_rays", "shadow_fetches", "primary_fetches", "ao_samples", "alg_bytes"):
-        assert a[k] == b[k], (k, a[k], b[k])
+    for i in (1, 2):
+        assert np.array_equal(outs[0], outs[i]), i
+        a, b = sts[0].as_dict(), sts[i].as_dict()
+        for k in ("shadow_rays", "shadow_fetches", "primary_fetches", "ao_samples", "alg_bytes"):
+            assert a[k] == b[k], (i, k, a[k], b[k])
 
 
 # ---- the reference's map.bin air encoding ------------------

@@ -28,6 +28,7 @@ FLAG_REFLECT, FLAG_ROUGH = 0x10, 0x20          # extensions
 FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
 FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary index path
 FLAG_SOFT_POOL = 0x80                           # soft shadows by the pooled wave march (same frames)
+FLAG_SOFT_BRICK = 0x100                         # + LDS 8^3 brick staging (same frames)
 MAX_SHADOW_SAMPLES = 16
 ABI_VERSION = 5
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin

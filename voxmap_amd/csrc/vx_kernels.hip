@@ -519,6 +519,64 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     return tv != 0;
 }
 
+// march_pad with an LDS brick (VX_FLAG_SOFT_BRICK, the EXT 4 instantiation:
+// north_star's "8^3 brick staging"): the pooled pass stages, per fragment, the
+// 8x8x8 block of the march channel around its start cell in LDS (origin at or
+// one cell behind the start on a positive axis, four to seven cells behind on a
+// negative one, x aligned to 4 bytes, so the first steps toward the sun stay
+// inside), and a step reads LDS when its cell lies in that brick, the global
+// channel otherwise.  Same step arithmetic as
+// march_pad (fract peel, exact cells), cells kept per axis for the brick test:
+// local = cell - origin as exact fp32 integers, inside iff the largest of the
+// three bit patterns is below bits(8.0f) (a negative local has its sign bit set).
+template <int SG>
+__device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S, const int8_t *sun,
+                                            const int8_t *brick, int ox, int oy, int oz, int c0, int c1, int c2,
+                                            float f0, float f1, float f2, unsigned &fetches, unsigned &witers) {
+    const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
+    const int maxs = a.fc.max_steps;
+    if (maxs <= 0) return maxs == 0;
+    constexpr float kBias = 8388608.0f;
+    const float xpf = (float)a.SXp;
+    const int8_t *sunb = sun - 0x4B000000;
+    float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB) + kBias;
+    // brick origin (padded cells, same biases as the cells)
+    const float b0 = (float)ox + kBias, b1 = (float)oy, b2 = (float)oz + kBias;
+    const unsigned sxpyp = a.SXpYp;
+    float len = march_len_sg<SG>(S, f0, f1, f2);
+    int tv = 1;
+    int step = 0;
+    bool first = true;
+    do {
+        const float safe = cvt_f32_ubyte0((uint32_t)tv);
+        f0 = f0 + (r0 * safe) * len;                                              // :118
+        f1 = f1 + (r1 * safe) * len;
+        f2 = f2 + (r2 * safe) * len;
+        const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
+        f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;                              // :120
+        e0 += fl0; e1 += fl1; e2 += fl2;                                          // :119
+        const float l0 = e0 - b0, l1 = e1 - b1, l2 = e2 - b2;                     // exact small integers
+        const unsigned m = max(max(__float_as_uint(l0), __float_as_uint(l1)), __float_as_uint(l2));
+        int t;
+        if (m < 0x41000000u) {                                                    // inside the brick
+            t = brick[(int)__builtin_fmaf(l2, 64.0f, __builtin_fmaf(l1, 8.0f, l0))];
+        } else {
+            const unsigned off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(__builtin_fmaf(e1, xpf, e0));
+            t = (int)ld_off(sunb, off);
+        }
+        len = first ? march_len_sg<SG>(S, f0, f1, f2)
+                    : (VX_FRACT ? march_len_fract<SG>(S, f0, f1, f2) : march_len_sg<SG>(S, f0, f1, f2));
+        first = false;
+        fetches += t >= 0 ? 1u : 0u;
+        tv = t;
+        witers += once_per_wave(1u);
+    } while (tv > 0 && ++step < maxs);
+    // lit: left the grid (-1), or the MAX_STEPS-th step taken whatever it read
+    // (render.frag:234: a block on the last step still ends with step == MAX_STEPS);
+    // a block found earlier ends the loop with step + 1 < maxs
+    return tv != 0 || step + 1 >= maxs;
+}
+
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
 __device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
@@ -902,7 +960,7 @@ __device__ __forceinline__ void normalize3(float v0, float v1, float v2, float &
 }
 
 // ---------------- render.frag main(), sky branch (render.frag:148-205) ----------------
-__device__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, float d1, float d2, float o[4],
+__device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, float d1, float d2, float o[4],
                           Counters &cnt) {
     const FrameConsts &F = a.fc;
     float r0, r1, r2;
@@ -1019,7 +1077,7 @@ __device__ float block_shade_factor(const KernelArgs &a, const float *unorm, con
 // lit_given >= 0 (EXT 2): the soft-shadow samples of this fragment were
 // marched by k_render's wave pass, lit_given of them lit.
 template <int EXT>
-__device__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt,
+__device__ __forceinline__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt,
                             bool has_ray = false, float q0 = 0.0f, float q1 = 0.0f, float q2 = 0.0f,
                             float *ray_out = nullptr, int lit_given = -1) {
     const FrameConsts &F = a.fc;
@@ -1364,8 +1422,9 @@ __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
     // EXT 3 (VX_FLAG_SOFT_POOL): the soft-shadow instantiation (EXT 2) with the
     // first surface's samples marched by the pooled wave pass
-    constexpr int XE = EXT == 3 ? 2 : EXT;
-    constexpr bool kPoolOn = EXT == 3 || (EXT == 2 && VX_POOL);
+    constexpr int XE = EXT >= 3 ? 2 : EXT;
+    constexpr bool kPoolOn = EXT >= 3 || (EXT == 2 && VX_POOL);
+    constexpr bool kBrick = EXT == 4;          // VX_FLAG_SOFT_BRICK: + LDS brick staging
     // LDS: [0, 256) unorm8 -> float table, b/255 as IEEE quotients (render.frag:38
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
@@ -1379,6 +1438,7 @@ void k_render(KernelArgs a) {
     __shared__ float4 s_pf[kPool ? kWG : 1];
     __shared__ int4 s_pc[kPool ? kWG : 1];
     __shared__ int s_plit[kPool ? kWG : 1];
+    __shared__ int s_brick[kBrick ? 4 * 4 * 128 : 1];      // per wave: 4 bricks of 8x8x8 int8 (dwords)
     if (kPool) {
         for (int k = 0; k < a.fc.n_sun; k++) {          // uniform k: scalar loads of the kernel argument
             if (threadIdx.x == k) {
@@ -1492,13 +1552,50 @@ void k_render(KernelArgs a) {
                 S.abs[0] = q1.x; S.abs[1] = q1.y; S.abs[2] = q1.z;
                 S.rcp[0] = q2.x; S.rcp[1] = q2.y; S.rcp[2] = q2.z;
                 const int8_t *ch = F.sun_k[0].up ? a.sunp : a.sunp + a.sunp_texels;
+                // EXT 4 is launched only when the bricks fit (launch_render): <= 4 fragments per
+                // pass, 4-byte aligned rows, a border of >= 9 cells around the grid
+                constexpr bool brick_on = kBrick;
+                const int sgv = F.soft_sg;
+                const int bx = (sgv & 1) ? 0 : 4, by = (sgv & 2) ? 1 : 6, bz = (sgv & 4) ? 1 : 6;
                 for (int base = 0; base < nf; base += 64 >> lg) {     // wave-uniform passes
                     const int fs = base + (lane >> lg);
+                    if (kBrick && brick_on) {
+                        // stage the pass's bricks: 4 x 64 rows x 2 dwords, 8 dword loads per lane
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        int *wbrick = s_brick + (wb >> 6) * 512;
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const int d = lane + 64 * j, bi = d >> 7, row = (d & 127) >> 1, half = d & 1;
+                            const int fb = min(base + bi, nf - 1);
+                            const int4 pc = s_pc[wb + fb];
+                            const int ox = (pc.x + a.SB - bx) & ~3, oy = pc.y + a.SB - by, oz = pc.z + a.SB - bz;
+                            const size_t off = (size_t)(unsigned)ox + 4u * half +
+                                               (size_t)(unsigned)a.SXp * (unsigned)(oy + (row & 7)) +
+                                               (size_t)a.SXpYp * (unsigned)(oz + (row >> 3));
+                            wbrick[d] = *reinterpret_cast<const int *>(ch + off);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                    }
                     if (klane && fs < nf) {
                         const float4 pf = s_pf[wb + fs];
                         const int4 pc = s_pc[wb + fs];
                         cnt.shadow_rays++;
                         bool lit;
+                        if (kBrick && brick_on) {
+                            const int8_t *br = reinterpret_cast<const int8_t *>(s_brick + (wb >> 6) * 512) +
+                                               512 * (lane >> lg);
+                            const int ox = (pc.x + a.SB - bx) & ~3, oy = pc.y + a.SB - by, oz = pc.z + a.SB - bz;
+                            switch (sgv) {
+#define VX_SGB(K) case K: lit = march_brick<K>(a, S, ch, br, ox, oy, oz, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
+                                               cnt.shadow_fetch, cnt.march_witers); break;
+                                VX_SGB(0) VX_SGB(1) VX_SGB(2) VX_SGB(3) VX_SGB(4) VX_SGB(5) VX_SGB(6)
+                                default: lit = march_brick<7>(a, S, ch, br, ox, oy, oz, pc.x, pc.y, pc.z, pf.x, pf.y,
+                                                              pf.z, cnt.shadow_fetch, cnt.march_witers);
+#undef VX_SGB
+                            }
+                        } else if constexpr (!kBrick)
                         switch (F.soft_sg) {
 #define VX_SGP(K) case K: lit = march_pad<K, false>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
                                                     cnt.shadow_fetch, cnt.march_witers, nullptr); break;
@@ -1737,10 +1834,13 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
         if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
         return (int)hipGetLastError();
     }
-    const int ext = a.fc.n_sun > 1 ? ((a.fc.flags & VX_FLAG_SOFT_POOL) ? 3 : 2)
+    const bool brick_ok = a.fc.soft_sg >= 0 && a.sunp && a.fc.soft_lg >= 4 && (a.SXp & 3) == 0 && a.SB >= 9;
+    const int ext = a.fc.n_sun > 1 ? ((a.fc.flags & VX_FLAG_SOFT_BRICK) && brick_ok ? 4
+                                      : (a.fc.flags & (VX_FLAG_SOFT_POOL | VX_FLAG_SOFT_BRICK)) ? 3 : 2)
                                    : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
 #define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
-#define VX_LE(F, S, T) do { if (ext == 3) VX_L(F, S, T, 3); else if (ext == 2) VX_L(F, S, T, 2); \
+#define VX_LE(F, S, T) do { if (ext == 4) VX_L(F, S, T, 4); else if (ext == 3) VX_L(F, S, T, 3); \
+                                else if (ext == 2) VX_L(F, S, T, 2); \
                                 else if (ext) VX_L(F, S, T, 1); else VX_L(F, S, T, 0); } while (0)
 #define VX_LT(F, S) do { if (tiled) VX_LE(F, S, true); else VX_LE(F, S, false); } while (0)
     if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_LT(0, true); else VX_LT(0, false); }

@@ -79,9 +79,12 @@ def check(lib: str) -> dict[str, dict[str, int]]:
     for name, v in render.items():
         p = render_params(name)
         stats = p is not None and p[1] == 1                        # STATS instantiation: counting only
+        # EXT 4 (VX_FLAG_SOFT_BRICK, an opt-in experiment): its 8 KB of LDS bricks
+        # cap it at 7 waves/SIMD anyway, so the compiler may use 73 VGPRs
+        brick = p is not None and p[3] == 4
         if v.get("private_segment_fixed_size", 0) > RENDER_SCRATCH_LIMIT:
             bad.append(f"{name}: private segment {v['private_segment_fixed_size']} B > {RENDER_SCRATCH_LIMIT}")
-        if not stats and v.get("vgpr_count", 0) > RENDER_VGPR_LIMIT:
+        if not stats and v.get("vgpr_count", 0) > (80 if brick else RENDER_VGPR_LIMIT):
             bad.append(f"{name}: {v['vgpr_count']} VGPRs > {RENDER_VGPR_LIMIT}")
     if bad:
         raise RuntimeError("render kernel resource check failed:\n  " + "\n  ".join(bad))
