@@ -17,16 +17,18 @@ def _render(meta):
 
 
 def test_every_render_instantiation_present(meta):
-    # FMT 2 x STATS 2 x TILED 2 x EXT mode 3 x primary index 2
-    assert len(_render(meta)) == 48
+    # FMT 2 x STATS 2 x TILED 2 x EXT mode 5 (v1, ext, soft, soft pooled, soft LDS bricks) x primary index 2
+    assert len(_render(meta)) == 80
 
 
 def test_render_kernels_fit_eight_waves_and_no_arg_copy(meta):
     from voxmap_amd import kernel_meta
     for p, v in _render(meta).items():
         assert v["private_segment_fixed_size"] <= kernel_meta.RENDER_SCRATCH_LIMIT, (p, v)
-        if not p[1]:                                   # timed (non-STATS) kernels
+        if not p[1] and p[3] != 4:                     # timed (non-STATS) kernels
             assert v["vgpr_count"] <= 64 and v["sgpr_count"] <= 80, (p, v)
+        elif not p[1]:                                 # EXT 4: LDS bricks hold it to 7 waves/SIMD anyway
+            assert v["vgpr_count"] <= 80, (p, v)
 
 
 def test_v1_kernel_has_no_spills(meta):
