@@ -356,7 +356,7 @@ __device__ __forceinline__ float march_len_fract(const SunRay &S, float f0, floa
     return len;
 }
 
-__device__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
+__device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
                            float f1, float f2, unsigned &fetches, unsigned &witers) {
     const FrameConsts &F = a.fc;
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
@@ -579,7 +579,7 @@ __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S
 
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
-__device__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
+__device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
                               float f1, float f2, unsigned &fetches, unsigned &witers) {
     const FrameConsts &F = a.fc;
     const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
@@ -670,7 +670,7 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, i
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <bool F32IDX>
-__device__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d2, Surf &g0, Surf &g1,
+__device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d2, Surf &g0, Surf &g1,
                        Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
@@ -834,7 +834,7 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
 }
 
 // sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G at LOD 0.
-__device__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
+__device__ __forceinline__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
     const FrameConsts &F = a.fc;
     int x0, x1, y0, y1, z0, z1;
     float wx, wy, wz;
@@ -895,7 +895,7 @@ __device__ __forceinline__ int wrap_idx(float fl, int n, float rn) {
 }
 
 // fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT, LOD 0.
-__device__ float fbm(const KernelArgs &a, const float *unorm, float px, float py) {
+__device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, float px, float py) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
@@ -1022,7 +1022,7 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unor
 
 // ---------------- extensions (DESIGN.md §3 "Extensions") ----------------
 // white(p) = 1 - 2*texture(u_noise, p).rgb (render.frag:16-21), bilinear REPEAT LOD 0.
-__device__ void white(const KernelArgs &a, const float *unorm, float px, float py, float &w0, float &w1, float &w2) {
+__device__ __forceinline__ void white(const KernelArgs &a, const float *unorm, float px, float py, float &w0, float &w1, float &w2) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
@@ -1055,7 +1055,7 @@ constexpr float kRoughAmp = 0.1f;
 // normal, exactly as shade_block computes it: the soft-shadow pass of k_render
 // asks it first, to know which fragments march.
 template <int EXT>
-__device__ float block_shade_factor(const KernelArgs &a, const float *unorm, const Surf &g) {
+__device__ __forceinline__ float block_shade_factor(const KernelArgs &a, const float *unorm, const Surf &g) {
     const FrameConsts &F = a.fc;
     const int ni = g.nidx;
     if (!(EXT && (F.flags & VX_FLAG_ROUGH))) return F.shadeFactor[ni];
@@ -1176,7 +1176,7 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const float *un
 // with glass_layer = 0).  Scalar form of primary(): reflection rays are few.
 // Returns 1 and the surface record, or 0 (sky: left the grid, or the start
 // cell is outside it).
-__device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o0, float o1, float o2, float d0,
+__device__ __forceinline__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o0, float o1, float o2, float d0,
                             float d1, float d2, int c0, int c1, int c2, Surf &h, Counters &cnt) {
     const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
     const uint32_t *pp = a.prim + (size_t)oct * a.copy_texels;
@@ -1239,7 +1239,7 @@ __device__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o
 // (rd = the camera rayDir at the fragment; R = rd with the face-axis
 // component negated = reflect(rd, n) exactly), oracle reflect_color().
 template <int EXT>
-__device__ void reflect_color(const KernelArgs &a, const float *unorm, const Surf &gl, const float rd[3], float out[3],
+__device__ __forceinline__ void reflect_color(const KernelArgs &a, const float *unorm, const Surf &gl, const float rd[3], float out[3],
                               Counters &cnt) {
     const int ax = gl.nidx >> 1;
     const float R0 = ax == 0 ? -rd[0] : rd[0], R1 = ax == 1 ? -rd[1] : rd[1], R2 = ax == 2 ? -rd[2] : rd[2];
@@ -1323,7 +1323,7 @@ __device__ __forceinline__ void primary_only_colour(int n, const Surf &g0, float
 // AO sample the reference also runs there do not reach the output (:244): not
 // run.  Oracle: vxo_render.c shade_2d.
 constexpr float kClear2d = 0.9f;
-__device__ void shade_2d(const KernelArgs &a, float d0, float d1, float d2, float rgba[4], Counters &cnt,
+__device__ __forceinline__ void shade_2d(const KernelArgs &a, float d0, float d1, float d2, float rgba[4], Counters &cnt,
                          unsigned &n_sky, unsigned &n_block, unsigned &n_glass) {
     const FrameConsts &F = a.fc;
     rgba[0] = rgba[1] = rgba[2] = kClear2d;
@@ -1557,7 +1557,8 @@ void k_render(KernelArgs a) {
                 constexpr bool brick_on = kBrick;
                 const int sgv = F.soft_sg;
                 const int bx = (sgv & 1) ? 0 : 4, by = (sgv & 2) ? 1 : 6, bz = (sgv & 4) ? 1 : 6;
-                for (int base = 0; base < nf; base += 64 >> lg) {     // wave-uniform passes
+                const int fpp = 64 >> lg;
+                for (int base = 0; base < nf; base += fpp) {          // wave-uniform passes
                     const int fs = base + (lane >> lg);
                     if (kBrick && brick_on) {
                         // stage the pass's bricks: 4 x 64 rows x 2 dwords, 8 dword loads per lane
