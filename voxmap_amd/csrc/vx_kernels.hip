@@ -25,8 +25,11 @@
 
 // Diagnostic padding (A/B only, never in the product build): VX_PAD_MARCH /
 // VX_PAD_PRIM extra independent v_add_f32 per loop iteration.
+// VX_RSTEP: the hard shadow's r*safe from a per-frame LDS table (round 1); off
+// since the typed SSCALED texel load (three multiplies on the loaded float are
+// off the LDS latency): C3 v1 -0.2 %, full quality -0.4 %.
 #ifndef VX_RSTEP
-#define VX_RSTEP 1
+#define VX_RSTEP 0
 #endif
 #ifndef VX_STOP_VGPR
 #define VX_STOP_VGPR 1
@@ -1428,7 +1431,7 @@ void k_render(KernelArgs a) {
     // LDS: [0, 256) unorm8 -> float table, b/255 as IEEE quotients (render.frag:38
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
     // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
-    __shared__ float4 s_lds[64 + 128];
+    __shared__ float4 s_lds[64 + (VX_RSTEP ? 128 : 0)];
     __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
     __shared__ float4 s_rk[XE == 2 && VX_SOFT_TAB ? 4 * 128 : 1];   // EXT 2: per wave, r*k of the current sample
     // EXT 2, VX_POOL: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
@@ -1453,7 +1456,7 @@ void k_render(KernelArgs a) {
 #pragma unroll
     for (int i = threadIdx.x; i < 256; i += kWG)        // = (float)i / 255.0f, the IEEE quotient (§5)
         s_unorm[i] = VX_UNORM_MK ? div_const((float)i, 255.0f, 1.0f / 255.0f) : (float)i / 255.0f;
-    if (threadIdx.x < 128) {
+    if (VX_RSTEP && threadIdx.x < 128) {
         const float k = (float)threadIdx.x;
         const SunRay &S0 = a.fc.sun_k[0];
         s_lds[64 + threadIdx.x] = make_float4(S0.r[0] * k, S0.r[1] * k, S0.r[2] * k, 0.0f);
