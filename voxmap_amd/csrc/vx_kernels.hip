@@ -260,6 +260,46 @@ __device__ __forceinline__ float ld_fmt_async(u32x4 rsrc, unsigned byte_off, flo
                  : "v"(byte_off), "s"(rsrc));
     return v;
 }
+// VX_TYPED_UNORM: texel channels decoded by the texture data unit.  A typed
+// buffer load with NUM_FORMAT UNORM returns RN(b / 255) for every byte b, the
+// exact render.frag:38 decode (tools/micro/unorm_check.hip: all 256 bytes, 8,
+// 8_8 and 8_8_8_8 formats, profiles/r02_unorm_check.txt), so the AO and noise
+// samples need no byte extraction and no LDS table read.  Loads are issued
+// together; one s_waitcnt tied to all their results comes before any use.
+#ifndef VX_TYPED_UNORM
+#define VX_TYPED_UNORM 1
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+#if VX_TYPED_UNORM
+__device__ __forceinline__ u32x4 unorm_rsrc(const void *base, unsigned w3) {
+    const unsigned long long p = (unsigned long long)base;
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((unsigned)p);
+    r.y = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32) & 0xffffu);
+    r.z = 0xffffffffu;
+    r.w = w3;
+    return r;
+}
+constexpr unsigned kRsrcRG = 0x1802Cu;     // 8_8, UNORM, dst (X, Y): (R, G) of a u16 R | G << 8
+constexpr unsigned kRsrcA = 0x50007u;      // 8_8_8_8, UNORM, dst X = W: the A channel
+constexpr unsigned kRsrcRGB = 0x501ACu;    // 8_8_8_8, UNORM, dst (X, Y, Z)
+__device__ __forceinline__ f32x2 ld_unorm2(u32x4 rsrc, unsigned off) {
+    f32x2 v;
+    asm volatile("buffer_load_format_xy %0, %1, %2, 0 offen" : "=&v"(v) : "v"(off), "s"(rsrc));
+    return v;
+}
+__device__ __forceinline__ float ld_unorm1(u32x4 rsrc, unsigned off) {
+    float v;
+    asm volatile("buffer_load_format_x %0, %1, %2, 0 offen" : "=&v"(v) : "v"(off), "s"(rsrc));
+    return v;
+}
+__device__ __forceinline__ f32x3 ld_unorm3(u32x4 rsrc, unsigned off) {
+    f32x3 v;
+    asm volatile("buffer_load_format_xyz %0, %1, %2, 0 offen" : "=&v"(v) : "v"(off), "s"(rsrc));
+    return v;
+}
+#endif
 __device__ __forceinline__ float ld_fmt(u32x4 rsrc, unsigned byte_off) {
     float v;
     asm("buffer_load_format_x %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(byte_off), "s"(rsrc));
@@ -851,6 +891,26 @@ __device__ __forceinline__ float sdf_lin(const KernelArgs &a, const float *unorm
     const unsigned dx = (unsigned)(x1 - x0) << 1, dy = __umul24((unsigned)(y1 - y0), 2u * (unsigned)a.X),
                    dz = __umul24((unsigned)(z1 - z0), 2u * a.XY);
     const unsigned b010 = b000 + dy, b001 = b000 + dz, b011 = b010 + dz;
+#if VX_TYPED_UNORM
+    const u32x4 rs = unorm_rsrc(a.rg, kRsrcRG);
+    f32x2 u000 = ld_unorm2(rs, b000), u100 = ld_unorm2(rs, b000 + dx), u010 = ld_unorm2(rs, b010);
+    f32x2 u110 = ld_unorm2(rs, b010 + dx), u001 = ld_unorm2(rs, b001), u101 = ld_unorm2(rs, b001 + dx);
+    f32x2 u011 = ld_unorm2(rs, b011), u111 = ld_unorm2(rs, b011 + dx);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(u000), "+v"(u100), "+v"(u010), "+v"(u110), "+v"(u001), "+v"(u101),
+                 "+v"(u011), "+v"(u111));
+    float ures[2];
+#pragma unroll
+    for (int ch = 0; ch < 2; ch++) {
+        const float v00 = gmix(u000[ch], u100[ch], wx);
+        const float v01 = gmix(u010[ch], u110[ch], wx);
+        const float v10 = gmix(u001[ch], u101[ch], wx);
+        const float v11 = gmix(u011[ch], u111[ch], wx);
+        const float w0 = gmix(v00, v01, wy);
+        const float w1 = gmix(v10, v11, wy);
+        ures[ch] = gmix(w0, w1, wz) * 255.0f;
+    }
+    return gmin(ures[0], ures[1]);
+#endif
     auto ld = [&](unsigned off) -> uint32_t { return (uint32_t)ld_off(a.rg, off); };
     const uint32_t t000 = ld(b000), t100 = ld(b000 + dx), t010 = ld(b010), t110 = ld(b010 + dx);
     const uint32_t t001 = ld(b001), t101 = ld(b001 + dx), t011 = ld(b011), t111 = ld(b011 + dx);
@@ -905,6 +965,13 @@ __device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, fl
     const float wa = u - fu, wb = v - fv;
     const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+#if VX_TYPED_UNORM
+    const u32x4 rs = unorm_rsrc(a.noise, kRsrcA);
+    auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
+    float t00 = ld_unorm1(rs, off(x0, y0)), t10 = ld_unorm1(rs, off(x1, y0));
+    float t01 = ld_unorm1(rs, off(x0, y1)), t11 = ld_unorm1(rs, off(x1, y1));
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(t00), "+v"(t10), "+v"(t01), "+v"(t11));
+#else
     // A byte of texel (x, y): byte 4*(y*W + x) + 3, W = 2^noise_lw
     auto ld = [&](int x, int y) -> uint32_t {
         return (uint32_t)ld_off(reinterpret_cast<const uint8_t *>(a.noise),
@@ -914,6 +981,7 @@ __device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, fl
     const float t10 = unorm[ld(x1, y0)];
     const float t01 = unorm[ld(x0, y1)];
     const float t11 = unorm[ld(x1, y1)];
+#endif
     const float r0 = gmix(t00, t10, wa), r1 = gmix(t01, t11, wa);
     return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
@@ -1032,11 +1100,24 @@ __device__ __forceinline__ void white(const KernelArgs &a, const float *unorm, f
     const float wa = u - fu, wb = v - fv;
     const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+    float w[3];
+#if VX_TYPED_UNORM
+    const u32x4 rs = unorm_rsrc(a.noise, kRsrcRGB);
+    auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
+    f32x3 u00 = ld_unorm3(rs, off(x0, y0)), u10 = ld_unorm3(rs, off(x1, y0));
+    f32x3 u01 = ld_unorm3(rs, off(x0, y1)), u11 = ld_unorm3(rs, off(x1, y1));
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(u00), "+v"(u10), "+v"(u01), "+v"(u11));
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const float r0 = gmix(u00[ch], u10[ch], wa);
+        const float r1 = gmix(u01[ch], u11[ch], wa);
+        w[ch] = 1.0f - 2.0f * gmix(r0, r1, wb);
+    }
+#else
     auto ld = [&](int x, int y) -> uint32_t {
         return ld_off(a.noise, (((unsigned)y << a.noise_lw) | (unsigned)x) << 2);
     };
     const uint32_t t00 = ld(x0, y0), t10 = ld(x1, y0), t01 = ld(x0, y1), t11 = ld(x1, y1);
-    float w[3];
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
         const int sh = 8 * ch;
@@ -1044,6 +1125,7 @@ __device__ __forceinline__ void white(const KernelArgs &a, const float *unorm, f
         const float r1 = gmix(unorm[(t01 >> sh) & 0xff], unorm[(t11 >> sh) & 0xff], wa);
         w[ch] = 1.0f - 2.0f * gmix(r0, r1, wb);
     }
+#endif
     w0 = w[0]; w1 = w[1]; w2 = w[2];
 }
 
