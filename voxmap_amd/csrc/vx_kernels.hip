@@ -169,22 +169,22 @@ struct Counters {
 
 // (float)((t >> 8k) & 0xff) as one v_cvt_f32_ubyteK (left to itself the
 // compiler may fold the mask away and emit a shift + convert)
-__device__ __forceinline__ float cvt_f32_ubyte0(uint32_t t) {
+[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte0(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
-__device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
+[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
-__device__ __forceinline__ float cvt_f32_ubyte2(uint32_t t) {
+[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte2(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
-__device__ __forceinline__ float cvt_f32_ubyte3(uint32_t t) {
+[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte3(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(t));
     return r;
@@ -210,7 +210,7 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 //   rg    R | G << 8, u16, linear: the AO trilinear sample.
 // Every read is in bounds: the traversal stays within P of the grid, march()
 // returns before reading outside it, the AO sample clamps.
-constexpr uint32_t kSentinel = 0xFFFFFFFFu;   // border cells: colour 0xFF, extents 255
+[[maybe_unused]] constexpr uint32_t kSentinel = 0xFFFFFFFFu;   // border cells: colour 0xFF, extents 255
 
 // Loads at a 32-bit byte offset from a wave-uniform base: lets the compiler
 // use the saddr form (SGPR base + VGPR offset) instead of 64-bit per-lane
@@ -269,9 +269,15 @@ __device__ __forceinline__ float ld_fmt_async(u32x4 rsrc, unsigned byte_off, flo
 #ifndef VX_TYPED_UNORM
 #define VX_TYPED_UNORM 1
 #endif
+// VX_PRIM_TYPED: the primary traversal's cell word through a typed USCALED
+// load (colour and extents as floats, no byte converts); parity-green and
+// measured +0.2..0.3 % on C3 (profiles/r02_ab_prim_typed_c3.txt): off.
+#ifndef VX_PRIM_TYPED
+#define VX_PRIM_TYPED 0
+#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x3 __attribute__((ext_vector_type(3)));
-#if VX_TYPED_UNORM
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 unorm_rsrc(const void *base, unsigned w3) {
     const unsigned long long p = (unsigned long long)base;
     u32x4 r;
@@ -281,6 +287,7 @@ __device__ __forceinline__ u32x4 unorm_rsrc(const void *base, unsigned w3) {
     r.w = w3;
     return r;
 }
+#if VX_TYPED_UNORM
 constexpr unsigned kRsrcRG = 0x1802Cu;     // 8_8, UNORM, dst (X, Y): (R, G) of a u16 R | G << 8
 constexpr unsigned kRsrcA = 0x50007u;      // 8_8_8_8, UNORM, dst X = W: the A channel
 constexpr unsigned kRsrcRGB = 0x501ACu;    // 8_8_8_8, UNORM, dst (X, Y, Z)
@@ -758,6 +765,31 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     const unsigned XpYp4 = 4u * a.XpYp;
     const unsigned kz = a.kz - XpYp4 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 2) - 0x4B000000u -
                         (XpYp4 << 22);
+#if VX_PRIM_TYPED
+    // the cell word through a typed load (8_8_8_8 USCALED, dst xyzw): colour and
+    // the three box extents arrive as exact fp32 integers, no byte converts in
+    // the loop; the colour logic runs on the float (the sentinel is 255.0)
+    // (F32IDX: the offset from a.prim carries the octant's copy; the integer
+    // path's per-lane copy base is no buffer base, so it converts the word)
+    const u32x4 prs = unorm_rsrc(a.prim, 0x52FACu);
+    auto fetch = [&](float x, float y, float z) -> f32x4 {
+        f32x4 v;
+        if (F32IDX) {
+            const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
+            const unsigned off = __umul24(__float_as_uint(z + 12582912.0f), XpYp4) + __float_as_uint(xy) + kz;
+            asm("buffer_load_format_xyzw %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(prs));
+        } else {
+            const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
+            const uint32_t w = ppad[(unsigned)idx];
+            v.x = cvt_f32_ubyte0(w); v.y = cvt_f32_ubyte1(w); v.z = cvt_f32_ubyte2(w); v.w = cvt_f32_ubyte3(w);
+        }
+        return v;
+    };
+    f32x4 t = fetch(h0, h1, h2);
+    cnt.prim_fetch++;
+    float prev = t.x;
+    float E0 = t.y, E1 = t.z, E2 = t.w;
+#else
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         if (F32IDX) {
             const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
@@ -771,11 +803,17 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     cnt.prim_fetch++;
     int prev = t & 0xff;
     float E0 = cvt_f32_ubyte1(t), E1 = cvt_f32_ubyte2(t), E2 = cvt_f32_ubyte3(t);
+#endif
     // gmark: the colour whose entry is "the first glass" -- glass until a glass
     // entry is recorded, then 256 (matches nothing).  The sentinel's colour
     // byte 0xFF is no vis colour (those are 0..21), so leaving the grid is an
     // entry that stops the walk.
+#if VX_PRIM_TYPED
+    float gmark = (float)kGlass, col;
+    int stop;
+#else
     int gmark = kGlass, stop, col;
+#endif
     float g0h = 0.0f, g1h = 0.0f, g2h = 0.0f, gt = 0.0f, te;
     float tb0, tb1, tb2;
     int gax = 0;
@@ -801,8 +839,13 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         h1 = e1 ? A1 + s1 : __builtin_amdgcn_fmed3f(q1, h1, A1);
         h2 = (!e0 && !e1) ? A2 + s2 : __builtin_amdgcn_fmed3f(q2, h2, A2);
         t = fetch(h0, h1, h2);
+#if VX_PRIM_TYPED
+        cnt.prim_fetch += t.x == 255.0f ? 0u : 1u;
+        col = t.x;
+#else
         cnt.prim_fetch += t >= kSentinel ? 0u : 1u;
         col = t & 0xff;
+#endif
         // a face of the mesh: entering a meshed cell (vis colour != 0) from a
         // cell of another colour; air is never meshed (sdf.cpp:229-233,284)
         const bool enter = col != prev && col != 0;
@@ -816,7 +859,11 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
 #endif
         prev = col;
+#if VX_PRIM_TYPED
+        E0 = t.y; E1 = t.z; E2 = t.w;
+#else
         E0 = cvt_f32_ubyte1(t); E1 = cvt_f32_ubyte2(t); E2 = cvt_f32_ubyte3(t);
+#endif
         cnt.prim_witers += once_per_wave(1u);      // counted in the loop: it stays a scalar
     } while (stop == 0 && ++it < cap);
     if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
@@ -824,7 +871,11 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     // masks (stop, tb == te) alive past it, at 3 SALU merges per mask per step
     asm volatile("" : "+v"(col), "+v"(stop), "+v"(tb0), "+v"(tb1), "+v"(te));
     if (stop == 0) cnt.cap_hit++;
+#if VX_PRIM_TYPED
+    const bool hit = stop != 0 && col != 255.0f;
+#else
     const bool hit = stop != 0 && t < kSentinel;
+#endif
     const int hax = tb0 == te ? 0 : (tb1 == te ? 1 : 2);    // exit axis of the last step (ties x < y < z)
     // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
     int nrec = 0;
@@ -849,7 +900,7 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         const int up = pos ? 0 : 1;
         const float r0 = h0 - hp0, r1 = h1 - hp1, r2 = h2 - hp2;
         h.id = col == kGlass ? 2 : 0;
-        h.color = col;
+        h.color = (int)col;
         h.nidx = 2 * hax + (pos ? 1 : 0);
         h.c0 = (int)r0 + cc0 + (hax == 0 ? up : 0);
         h.c1 = (int)r1 + cc1 + (hax == 1 ? up : 0);
