@@ -272,6 +272,9 @@ __device__ __forceinline__ float ld_fmt_async(u32x4 rsrc, unsigned byte_off, flo
 // VX_PRIM_TYPED: the primary traversal's cell word through a typed USCALED
 // load (colour and extents as floats, no byte converts); parity-green and
 // measured +0.2..0.3 % on C3 (profiles/r02_ab_prim_typed_c3.txt): off.
+#ifndef VX_SKY_BATCH
+#define VX_SKY_BATCH 1
+#endif
 #ifndef VX_PRIM_TYPED
 #define VX_PRIM_TYPED 0
 #endif
@@ -1009,6 +1012,33 @@ __device__ __forceinline__ int wrap_idx(float fl, int n, float rn) {
 }
 
 // fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT, LOD 0.
+#if VX_TYPED_UNORM
+// fbm in two halves, so the sky's four independent fbm samples (render.frag:
+// 188-189, 196-197) have all their typed loads in flight before one wait:
+// fbm_issue starts the four A-texel loads and keeps the bilinear weights,
+// fbm_finish (after a wait tied to t[]) blends them -- the same arithmetic as fbm.
+struct FbmTap {
+    float t[4];
+    float wa, wb;
+};
+__device__ __forceinline__ void fbm_issue(const KernelArgs &a, float px, float py, FbmTap &q) {
+    const int W = a.noise_w, H = a.noise_h;
+    const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
+    const float fu = floorf(u), fv = floorf(v);
+    q.wa = u - fu; q.wb = v - fv;
+    const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
+    const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
+    const u32x4 rs = unorm_rsrc(a.noise, kRsrcA);
+    auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
+    q.t[0] = ld_unorm1(rs, off(x0, y0)); q.t[1] = ld_unorm1(rs, off(x1, y0));
+    q.t[2] = ld_unorm1(rs, off(x0, y1)); q.t[3] = ld_unorm1(rs, off(x1, y1));
+}
+__device__ __forceinline__ float fbm_finish(const FbmTap &q) {
+    const float r0 = gmix(q.t[0], q.t[1], q.wa), r1 = gmix(q.t[2], q.t[3], q.wa);
+    return 1.0f - 2.0f * gmix(r0, r1, q.wb);
+}
+#define VX_WAIT_TAPS(Q) "+v"(Q.t[0]), "+v"(Q.t[1]), "+v"(Q.t[2]), "+v"(Q.t[3])
+#endif
 __device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, float px, float py) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
@@ -1119,6 +1149,25 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unor
     sx = sx * 0.1f; sy = sy * 0.1f;
     const float sl = sqrtf(sqrtf(sx * sx + sy * sy));
     sx = sx * sl; sy = sy * sl;
+#if VX_TYPED_UNORM && VX_SKY_BATCH
+    // the four samples that do not depend on another fbm: 16 loads, one wait
+    const float mountainPos = r0 / r1;                                            // :195
+    FbmTap q0, q1, q3, q4;
+    fbm_issue(a, 2.0f * sx + ct, 2.0f * sy + ct, q0);
+    fbm_issue(a, 2.0f * sx - ct, 2.0f * sy - ct, q1);
+    fbm_issue(a, 0.3f * mountainPos, 0.3f * mountainPos, q3);
+    fbm_issue(a, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2), q4);
+    asm volatile("s_waitcnt vmcnt(0)" : VX_WAIT_TAPS(q0), VX_WAIT_TAPS(q1), VX_WAIT_TAPS(q3), VX_WAIT_TAPS(q4));
+    const float n0 = fbm_finish(q0);
+    const float n1 = fbm_finish(q1);
+    sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
+    sx = sx + F.skyOff[0];
+    sy = sy + F.skyOff[1];
+    const float cloudFactor = vexp2(6.0f * (fbm(a, unorm, sx + 2.0f * ct, sy + -9.0f * ct) - 1.0f));
+    const float scf = sqrtf(cloudFactor);
+    float mountainHeight = 1.0f - fbm_finish(q3);
+    const float mountainFactor = 2.0f - fbm_finish(q4);
+#else
     const float n0 = fbm(a, unorm, 2.0f * sx + ct, 2.0f * sy + ct);
     const float n1 = fbm(a, unorm, 2.0f * sx - ct, 2.0f * sy - ct);
     sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
@@ -1129,6 +1178,7 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unor
     const float mountainPos = r0 / r1;                                            // :195
     float mountainHeight = 1.0f - fbm(a, unorm, 0.3f * mountainPos, 0.3f * mountainPos);
     const float mountainFactor = 2.0f - fbm(a, unorm, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2));
+#endif
     mountainHeight = mountainHeight / (vexp(0.3f * mountainPos * mountainPos) * 6.0f);
     if (mountainHeight > r2 && r1 > 0.0f && r2 > 0.0f) {
         const float mt[3] = {0.7f, 0.8f, 0.7f};
