@@ -264,16 +264,18 @@ __device__ __forceinline__ float ld_fmt_async(u32x4 rsrc, unsigned byte_off, flo
 // buffer load with NUM_FORMAT UNORM returns RN(b / 255) for every byte b, the
 // exact render.frag:38 decode (tools/micro/unorm_check.hip: all 256 bytes, 8,
 // 8_8 and 8_8_8_8 formats, profiles/r02_unorm_check.txt), so the AO and noise
-// samples need no byte extraction and no LDS table read.  Loads are issued
-// together; one s_waitcnt tied to all their results comes before any use.
+// samples need no byte extraction and no LDS table read.
 #ifndef VX_TYPED_UNORM
 #define VX_TYPED_UNORM 1
 #endif
 // VX_PRIM_TYPED: the primary traversal's cell word through a typed USCALED
 // load (colour and extents as floats, no byte converts); parity-green and
 // measured +0.2..0.3 % on C3 (profiles/r02_ab_prim_typed_c3.txt): off.
+// VX_SKY_BATCH: the sky's four independent fbm loads placed first by hand; with
+// the compiler-visible typed loads its own schedule is better (C3 full -0.9 %
+// without it, profiles/r02_ab_unorm_intrinsics.txt): off
 #ifndef VX_SKY_BATCH
-#define VX_SKY_BATCH 1
+#define VX_SKY_BATCH 0
 #endif
 #ifndef VX_PRIM_TYPED
 #define VX_PRIM_TYPED 0
@@ -294,21 +296,18 @@ __device__ __forceinline__ u32x4 unorm_rsrc(const void *base, unsigned w3) {
 constexpr unsigned kRsrcRG = 0x1802Cu;     // 8_8, UNORM, dst (X, Y): (R, G) of a u16 R | G << 8
 constexpr unsigned kRsrcA = 0x50007u;      // 8_8_8_8, UNORM, dst X = W: the A channel
 constexpr unsigned kRsrcRGB = 0x501ACu;    // 8_8_8_8, UNORM, dst (X, Y, Z)
-__device__ __forceinline__ f32x2 ld_unorm2(u32x4 rsrc, unsigned off) {
-    f32x2 v;
-    asm volatile("buffer_load_format_xy %0, %1, %2, 0 offen" : "=&v"(v) : "v"(off), "s"(rsrc));
-    return v;
-}
-__device__ __forceinline__ float ld_unorm1(u32x4 rsrc, unsigned off) {
-    float v;
-    asm volatile("buffer_load_format_x %0, %1, %2, 0 offen" : "=&v"(v) : "v"(off), "s"(rsrc));
-    return v;
-}
-__device__ __forceinline__ f32x3 ld_unorm3(u32x4 rsrc, unsigned off) {
-    f32x3 v;
-    asm volatile("buffer_load_format_xyz %0, %1, %2, 0 offen" : "=&v"(v) : "v"(off), "s"(rsrc));
-    return v;
-}
+// the LLVM typed-load intrinsics themselves: the compiler sees the loads, so it
+// places the waits, schedules them freely and never spills a register a load
+// has not written yet
+__device__ float vx_ld_format_f32(u32x4 rsrc, unsigned voff, int soff, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.format.f32");
+__device__ f32x2 vx_ld_format_v2f32(u32x4 rsrc, unsigned voff, int soff, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.format.v2f32");
+__device__ f32x3 vx_ld_format_v3f32(u32x4 rsrc, unsigned voff, int soff, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.format.v3f32");
+__device__ __forceinline__ f32x2 ld_unorm2(u32x4 rsrc, unsigned off) { return vx_ld_format_v2f32(rsrc, off, 0, 0); }
+__device__ __forceinline__ float ld_unorm1(u32x4 rsrc, unsigned off) { return vx_ld_format_f32(rsrc, off, 0, 0); }
+__device__ __forceinline__ f32x3 ld_unorm3(u32x4 rsrc, unsigned off) { return vx_ld_format_v3f32(rsrc, off, 0, 0); }
 #endif
 __device__ __forceinline__ float ld_fmt(u32x4 rsrc, unsigned byte_off) {
     float v;
@@ -950,8 +949,6 @@ __device__ __forceinline__ float sdf_lin(const KernelArgs &a, const float *unorm
     f32x2 u000 = ld_unorm2(rs, b000), u100 = ld_unorm2(rs, b000 + dx), u010 = ld_unorm2(rs, b010);
     f32x2 u110 = ld_unorm2(rs, b010 + dx), u001 = ld_unorm2(rs, b001), u101 = ld_unorm2(rs, b001 + dx);
     f32x2 u011 = ld_unorm2(rs, b011), u111 = ld_unorm2(rs, b011 + dx);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(u000), "+v"(u100), "+v"(u010), "+v"(u110), "+v"(u001), "+v"(u101),
-                 "+v"(u011), "+v"(u111));
     float ures[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
@@ -1012,11 +1009,11 @@ __device__ __forceinline__ int wrap_idx(float fl, int n, float rn) {
 }
 
 // fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT, LOD 0.
-#if VX_TYPED_UNORM
+#if VX_TYPED_UNORM && VX_SKY_BATCH
 // fbm in two halves, so the sky's four independent fbm samples (render.frag:
-// 188-189, 196-197) have all their typed loads in flight before one wait:
-// fbm_issue starts the four A-texel loads and keeps the bilinear weights,
-// fbm_finish (after a wait tied to t[]) blends them -- the same arithmetic as fbm.
+// 188-189, 196-197) issue all their typed loads first: fbm_issue starts the
+// four A-texel loads and keeps the bilinear weights, fbm_finish blends them --
+// the same arithmetic as fbm.
 struct FbmTap {
     float t[4];
     float wa, wb;
@@ -1037,7 +1034,6 @@ __device__ __forceinline__ float fbm_finish(const FbmTap &q) {
     const float r0 = gmix(q.t[0], q.t[1], q.wa), r1 = gmix(q.t[2], q.t[3], q.wa);
     return 1.0f - 2.0f * gmix(r0, r1, q.wb);
 }
-#define VX_WAIT_TAPS(Q) "+v"(Q.t[0]), "+v"(Q.t[1]), "+v"(Q.t[2]), "+v"(Q.t[3])
 #endif
 __device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, float px, float py) {
     const int W = a.noise_w, H = a.noise_h;
@@ -1051,7 +1047,6 @@ __device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, fl
     auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
     float t00 = ld_unorm1(rs, off(x0, y0)), t10 = ld_unorm1(rs, off(x1, y0));
     float t01 = ld_unorm1(rs, off(x0, y1)), t11 = ld_unorm1(rs, off(x1, y1));
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(t00), "+v"(t10), "+v"(t01), "+v"(t11));
 #else
     // A byte of texel (x, y): byte 4*(y*W + x) + 3, W = 2^noise_lw
     auto ld = [&](int x, int y) -> uint32_t {
@@ -1150,14 +1145,13 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unor
     const float sl = sqrtf(sqrtf(sx * sx + sy * sy));
     sx = sx * sl; sy = sy * sl;
 #if VX_TYPED_UNORM && VX_SKY_BATCH
-    // the four samples that do not depend on another fbm: 16 loads, one wait
+    // the four samples that do not depend on another fbm: their 16 loads first
     const float mountainPos = r0 / r1;                                            // :195
     FbmTap q0, q1, q3, q4;
     fbm_issue(a, 2.0f * sx + ct, 2.0f * sy + ct, q0);
     fbm_issue(a, 2.0f * sx - ct, 2.0f * sy - ct, q1);
     fbm_issue(a, 0.3f * mountainPos, 0.3f * mountainPos, q3);
     fbm_issue(a, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2), q4);
-    asm volatile("s_waitcnt vmcnt(0)" : VX_WAIT_TAPS(q0), VX_WAIT_TAPS(q1), VX_WAIT_TAPS(q3), VX_WAIT_TAPS(q4));
     const float n0 = fbm_finish(q0);
     const float n1 = fbm_finish(q1);
     sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
@@ -1207,7 +1201,6 @@ __device__ __forceinline__ void white(const KernelArgs &a, const float *unorm, f
     auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
     f32x3 u00 = ld_unorm3(rs, off(x0, y0)), u10 = ld_unorm3(rs, off(x1, y0));
     f32x3 u01 = ld_unorm3(rs, off(x0, y1)), u11 = ld_unorm3(rs, off(x1, y1));
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(u00), "+v"(u10), "+v"(u01), "+v"(u11));
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
         const float r0 = gmix(u00[ch], u10[ch], wa);
