@@ -6,18 +6,27 @@ C3: 3840x2160 "full quality" = the reference's v1 shading (primary visibility +
 sun march + AO + sky/clouds + glass) + the f-3 extensions reflection and rough
 normals, on the synthetic S-proc 1024x256x32 field, camera K1, the reference's
 own res/noise.bin.gz) from the HBM-resident field into an HBM-resident RGBA8
-framebuffer.  In the same N = 1 run: the v1 shading alone (config.v1) and
+framebuffer.  In the same N = 1 run: the v1 shading alone (config.v1),
 BASELINE configs[4] C5 (3^3-upscaled 3072x768x96 field, 16-sample soft
-shadows; config.c5).  --config C5 makes C5 the headline.
+shadows; config.c5) and the frame rate with the framebuffer copied to pinned
+host memory (config.fps_with_d2h, SURVEY §8d: kernel + D2H).  --config C5
+makes C5 the headline.
 
-N > 1 GPUs (one process per GPU, torchrun): the frame is cut into 64-row
-full-width bands dealt round-robin; each rank renders its bands in place and
-rank 0 gathers them into its frame over RCCL (vx_mgpu_render: native C++,
-ncclSend/ncclRecv in one group; --gather torch runs the same protocol through
-torch.distributed).  The gather is inside the timed step.  --config C3 (the
-driver's default): weak scaling, the frame grows with N (3840*sqrt(N) x
-2160*sqrt(N)); --config C4: BASELINE configs[3], 7680x4320 for every N
-(strong scaling).
+N > 1 GPUs, one process per GPU: launched by torch.distributed.run, or by
+``python bench.py --gpus N`` itself, which starts N rank processes (fresh
+interpreters, before anything touches a GPU) and exits with their status.  The
+frame is cut into 64-row full-width bands dealt round-robin; each rank renders
+its bands in place and rank 0 gathers them into its frame over RCCL
+(vx_mgpu_render: native C++, ncclSend/ncclRecv in one group; --gather torch
+runs the same protocol through torch.distributed).  The gather is inside the
+timed step.  The default config for N > 1 is BASELINE configs[3], C4:
+7680x4320 for every N (strong scaling); --config C3 grows the frame with N
+instead (3840*sqrt(N) x 2160*sqrt(N), weak scaling).
+
+--standin (tests only): the same orchestration (rank spawn, barriers, band
+deal, gather, max-over-ranks timing, the JSON line) on CPU over gloo, with a
+stand-in band renderer instead of the HIP library -- what
+tests/test_bench_spawn.py runs.
 
 Prints ONE JSON line on rank 0.
 """
@@ -27,6 +36,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,7 +48,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table
 BAND = 64               # rows per band of the multi-GPU deal
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -49,11 +60,13 @@ def parse():
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed frames rendered before the warmup so the GPU clock leaves its idle state "
                          "(a ~5 ms burst runs ~12%% slower than steady state: profiles/r01_clock_settle.txt)")
-    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--config", default=None, choices=["C2", "C3", "C4", "C5"],
+                    help="default: C3 on one GPU, C4 (7680x4320, BASELINE configs[3]) on N > 1")
     ap.add_argument("--camera", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 measurement of an N = 1 C3 run")
+    ap.add_argument("--no-d2h", action="store_true", help="skip the kernel + D2H frame rate of an N = 1 run")
     ap.add_argument("--quality", choices=["full", "v1"], default="full",
                     help="full = v1 + REFLECT + ROUGH (BASELINE 'full quality'); v1 = the reference shader only")
     ap.add_argument("--flags", type=int, default=None, help="VX_FLAG_* bits overriding --quality (diagnostics)")
@@ -62,49 +75,82 @@ def parse():
     ap.add_argument("--gather", choices=["native", "torch"], default="native",
                     help="N > 1: native = vx_mgpu_render (RCCL from C++); torch = the same bands over "
                          "torch.distributed 'nccl'")
-    return ap.parse_args()
+    ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
 
-def frame_size(cfg_name, cfg, world):
-    """(W, H, scaling) of the run: C4 fixed (strong), else grown by sqrt(N) (weak)."""
-    if cfg_name == "C4" or world == 1:
-        return cfg["w"], cfg["h"], ("strong" if cfg_name == "C4" and world > 1 else "weak")
-    s = math.sqrt(world)
-    return int(round(cfg["w"] * s / 32)) * 32, int(round(cfg["h"] * s / 8)) * 8, "weak"
+# ---------------------------------------------------------------- rank spawn
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def timed(torch, step, steps, warmup, settle_ms, dist=None):
+def spawn_ranks(n: int, argv) -> int:
+    """``bench.py --gpus N`` without a launcher: start N rank processes of this
+    script (fresh interpreters: nothing in this process has touched a GPU, and
+    nothing is exec'd), the torch.distributed.run environment set for each,
+    and return the first non-zero exit status.  Rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait()
+            if code and not rc:
+                rc = code
+                for q in procs:                 # one rank failed: the others would wait at a barrier forever
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+# ---------------------------------------------------------------- timing
+def timed(sync, step, steps, warmup, settle_ms, dist=None, sync_dev=None):
     """Settle the clock, warm up, then time `steps` frames bracketed by a barrier
     and a device synchronise on both sides (max over ranks taken by the caller)."""
+    import torch
     settle = 0
     if settle_ms > 0:
-        torch.cuda.synchronize()
+        sync()
         tp = time.perf_counter()
         for _ in range(3):
             step()
-        torch.cuda.synchronize()
+        sync()
         probe_ms = 1000.0 * (time.perf_counter() - tp) / 3
         n = torch.tensor([math.ceil(settle_ms / max(probe_ms, 1e-3))], dtype=torch.int64)
         if dist is not None:
-            if dist.get_backend() == "nccl":
-                n = n.cuda()
+            if sync_dev is not None:
+                n = n.to(sync_dev)
             dist.all_reduce(n, op=dist.ReduceOp.MAX)     # equal frame counts: the step is collective
         settle = int(min(int(n.item()), 20000)) + 3
         for _ in range(settle - 3):
             step()
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     return time.perf_counter() - t0, settle
 
 
@@ -151,9 +197,53 @@ def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms):
     def step():
         fns[n[0] % K]()
         n[0] += 1
-    wall, settle = timed(torch, step, steps, warmup, settle_ms)
+    wall, settle = timed(torch.cuda.synchronize, step, steps, warmup, settle_ms)
     ev = event_ms(torch, fns[0], steps)
     return {"wall_s": wall, "settle": settle, "ev_ms": ev, "stats": st.as_dict()}
+
+
+def fps_with_d2h(torch, vx, scene, frame, W, H, frames, K=2):
+    """SURVEY §8d's fps: kernel + the RGBA8 framebuffer copied to pinned host
+    memory.  K framebuffers; frame i renders into fb[i % K] on the render stream
+    and is copied out on a second stream while frame i + 1 renders (the render
+    into fb[j] waits for that buffer's previous copy)."""
+    rs, cs = torch.cuda.Stream(), torch.cuda.Stream()
+    fbs = [torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") for _ in range(K)]
+    hosts = [torch.empty(H * W * 4, dtype=torch.uint8, pin_memory=True) for _ in range(K)]
+    copied = [None] * K
+
+    def one(i):
+        j = i % K
+        if copied[j] is not None:
+            rs.wait_event(copied[j])
+        scene.render_device(frame, fbs[j].data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=rs.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(rs)
+        cs.wait_event(done)
+        with torch.cuda.stream(cs):
+            hosts[j].copy_(fbs[j], non_blocking=True)
+        copied[j] = torch.cuda.Event()
+        copied[j].record(cs)
+    for i in range(4):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(frames):
+        one(i)
+    torch.cuda.synchronize()
+    ms = 1000.0 * (time.perf_counter() - t0) / frames
+    # the copy alone (one stream, same bytes) to show what binds
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(frames):
+        hosts[i % K].copy_(fbs[i % K], non_blocking=True)
+    torch.cuda.synchronize()
+    copy_ms = 1000.0 * (time.perf_counter() - t1) / frames
+    return {"fps": round(1000.0 / ms, 2), "ms_per_frame": round(ms, 4), "frames": frames,
+            "d2h_bytes_per_frame": H * W * 4, "d2h_alone_ms": round(copy_ms, 4),
+            "d2h_gbps": round(H * W * 4 / (copy_ms * 1e-3) / 1e9, 2),
+            "how": f"{K} framebuffers; render on one stream, RGBA8 copy to pinned host memory on a second, "
+                   "overlapped with the next frame's render"}
 
 
 def roofline_of(alg_bytes, ms):
@@ -161,150 +251,216 @@ def roofline_of(alg_bytes, ms):
     return achieved, achieved / HBM_PEAK_GBPS
 
 
-def main():
-    args = parse()
+def lane_utils(s):
+    """Wave-loop lane utilisations from the STATS counters (each <= 1)."""
+    return {"primary": round(s["primary_fetches"] / max(1, 64 * s["primary_wave_iters"]), 4),
+            "march": round(s["shadow_fetches"] / max(1, 64 * s["march_wave_iters"]), 4),
+            "march_marching_lanes": round(s["shadow_fetches"] / max(1, s["march_lane_slots"]), 4),
+            "how": "fetches / (64 x wave loop iterations); march_marching_lanes: over the lanes that began "
+                   "each march (idle lanes of sky / unlit pixels excluded)"}
+
+
+# ---------------------------------------------------------------- N > 1
+def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local, standin):
+    """Bands dealt round-robin, rendered in place, gathered to rank 0; timed max over ranks."""
+    dev = "cpu" if standin else "cuda"
+    sync = (lambda: None) if standin else torch.cuda.synchronize
+    mg = split_ms = None
+    if standin:
+        streams = [None] * K
+    else:
+        streams = [torch.cuda.Stream() for _ in range(K)]
+        torch.cuda.set_stream(streams[0])
+    frames = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(K)]
+    group = None
+    gather = args.gather
+    if standin:
+        gather = "torch"
+    elif gather == "native":
+        uid = [vx.mgpu_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        try:
+            mg = vx.MultiGPU(scene, uid[0], world, rank)
+            ok = torch.tensor([1])
+        except Exception as e:          # RCCL init refused: fall back to the torch-driven gather
+            print(f"rank {rank}: vx_mgpu_create failed ({e}); falling back to --gather torch", file=sys.stderr)
+            mg, ok = None, torch.tensor([0])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if mg is not None:
+                mg.close()
+                mg = None
+            gather = "torch-fallback"
+            group = dist.new_group(list(range(world)), backend="nccl")
+    if gather == "native":
+        fns = [(lambda fb=frames[j], sj=streams[j].cuda_stream:
+                mg.render(frame, BAND, fb.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
+        st = mg.render(frame, BAND, frames[0].data_ptr(), pixel_format=vx.PIXEL_RGBA8,
+                       stream=streams[0].cuda_stream, stats=True).as_dict()
+        gather_desc = "vx_mgpu_render: one RCCL ncclSend/ncclRecv group into rank 0's frame rows (native C++)"
+    else:
+        from voxmap_amd.dist import BandGather, band_rows_of
+        gs = []
+        for j in range(K):
+            if standin:
+                def rb(ids, fr, j=j):                  # stand-in renderer: each band filled from its id
+                    for b in ids:
+                        fr[band_rows_of(b, H, BAND)] = (b * 7 + j) % 251
+            else:
+                def rb(ids, fr, sj=streams[j].cuda_stream):
+                    scene.render_bands(frame, BAND, ids, fr.data_ptr(), inplace=True, stream=sj)
+            g = BandGather(dist, W, H, BAND, 4, torch.uint8, dev, rb, group=group)
+            g.frame = frames[j]
+            gs.append(g)
+
+        def mk(j):
+            def f():
+                if standin:
+                    gs[j].step()
+                else:
+                    with torch.cuda.stream(streams[j]):
+                        gs[j].step()
+            return f
+        fns = [mk(j) for j in range(K)]
+        if standin:
+            gs[0].step()
+            st = {"pixels": W * sum(band_rows_of(b, H, BAND).stop - band_rows_of(b, H, BAND).start
+                                    for b in gs[0].mine), "shadow_rays": 0, "reflect_rays": 0, "alg_bytes": 0,
+                  "kernel_ms": 0.0}
+        else:
+            st = scene.render_bands(frame, BAND, gs[0].mine, frames[0].data_ptr(), inplace=True,
+                                    stream=streams[0].cuda_stream, stats=True).as_dict()
+        gather_desc = ("torch.distributed batch_isend_irecv into rank 0's frame rows" +
+                       (" (fallback: vx_mgpu_create failed)" if group is not None else "") +
+                       (" (gloo, CPU stand-in renderer)" if standin else " (RCCL)"))
+    keys = [k for k in st.keys() if k != "kernel_ms"]
+    vec = torch.tensor([float(st[k]) for k in keys], dtype=torch.float64)
+    on_dev = gather == "torch" and not standin
+    if on_dev:
+        vec = vec.cuda()
+    dist.all_reduce(vec)
+    stats = {k: float(v) for k, v in zip(keys, vec.cpu().tolist())}
+    stats["kernel_ms"] = float(st["kernel_ms"])
+    n = [0]
+
+    def step():
+        fns[n[0] % K]()
+        n[0] += 1
+    wall, settle_steps = timed(sync, step, args.steps, args.warmup, 0.0 if standin else args.settle_ms, dist,
+                               "cuda" if on_dev else None)
+    tt = torch.tensor([wall], dtype=torch.float64)
+    if on_dev:
+        tt = tt.cuda()
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    wall = float(tt.item())
+    if rank == 0 and standin:
+        # the gathered frame must hold every band's stand-in value
+        from voxmap_amd.dist import band_rows_of as bro
+        j_last = (n[0] - 1) % K
+        good = all(int(frames[j_last][bro(b, H, BAND)][0, 0, 0]) == (b * 7 + j_last) % 251
+                   for b in range(-(-H // BAND)))
+        stats["standin_frame_ok"] = bool(good)
+    if mg is not None:
+        # SURVEY §8e: render and gather timed apart (one stream, one frame at a
+        # time, max over ranks): vx_render_bands of this rank's bands, then
+        # vx_mgpu_gather alone (collective)
+        try:
+            mine = vx.mgpu_bands(H, BAND, world, rank)
+            s0 = streams[0].cuda_stream
+
+            def r_only():
+                if mine:
+                    scene.render_bands(frame, BAND, mine, frames[0].data_ptr(), inplace=True, stream=s0)
+
+            def g_only():
+                mg.gather(W, H, BAND, frames[0].data_ptr(), stream=s0)
+            tr, _ = timed(sync, r_only, args.steps, 2, 0.0, dist)
+            tg, _ = timed(sync, g_only, args.steps, 2, 0.0, dist)
+            t2 = torch.tensor([tr, tg], dtype=torch.float64)
+            dist.all_reduce(t2, op=dist.ReduceOp.MAX)
+            split_ms = {"render_ms": round(1000.0 * float(t2[0]) / args.steps, 4),
+                        "gather_ms": round(1000.0 * float(t2[1]) / args.steps, 4),
+                        "gather_bytes": int(sum(x[5] for x in vx.mgpu_transfers(W, H, BAND, world, 0))),
+                        "how": "one stream, one frame at a time, max over ranks (the timed step overlaps "
+                               "frames in flight, so it is less than the sum)"}
+        except Exception as e:            # never let the diagnostic break the bench line
+            split_ms = {"error": str(e)}
+        mg.close()
+    shards = {"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
+              "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc, "split_ms": split_ms}
+    return stats, wall, settle_steps, shards
+
+
+# ---------------------------------------------------------------- main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, argv)
     import torch
     import torch.distributed as dist
 
-    import voxmap_amd as vx
-    from voxmap_amd import presets, scenes
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = max(int(os.environ.get("WORLD_SIZE", "1")), 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus > 1 and world == 1:
-        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    world = max(world, 1)
-    torch.cuda.set_device(local)
+    standin = args.standin
     if world > 1:
         # native gather: RCCL lives in libvoxmap_hip.so; torch.distributed (gloo) only
         # shares the RCCL unique id, holds the barriers and takes the max time
-        if args.gather == "torch":
+        if args.gather == "torch" and not standin:
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    if not standin:
+        torch.cuda.set_device(local)
+    import voxmap_amd as vx
+    from voxmap_amd import presets, scenes
 
-    cfg = presets.CONFIGS[args.config]
+    cfg_name = args.config or ("C3" if world == 1 else "C4")
+    cfg = presets.CONFIGS[cfg_name]
     cam = args.camera or cfg["camera"]
-    W, H, scaling = frame_size(args.config, cfg, world)
+    if cfg_name == "C4" or world == 1:
+        W, H = cfg["w"], cfg["h"]
+        scaling = "strong" if world > 1 else "weak"
+    else:
+        s = math.sqrt(world)
+        W, H, scaling = int(round(cfg["w"] * s / 32)) * 32, int(round(cfg["h"] * s / 8)) * 8, "weak"
+    if standin:
+        W, H = min(W, 256), min(H, 200)
     up = 3.0 if cfg["scene"] == "s_up3" else 1.0
-
-    grid = presets.scene_grid(cfg["scene"])
-    Z, Y, X = grid.shape
-    noise = scenes.real_noise()            # the reference's res/noise.bin.gz (u_noise, render.js:138)
-    t_scene = time.perf_counter()
-    # palette grid in, distance field + octant copies built on the device (f-1);
-    # the noise texture through the product's .gz loader
-    scene = vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_path=scenes.NOISE_PATH,
-                     dims=(X, Y, Z), device=local)
-    t_scene = time.perf_counter() - t_scene
-    del grid
     flags = args.flags if args.flags is not None else (vx.FLAG_FULL_QUALITY if args.quality == "full" else 0)
     samples = args.samples if args.samples is not None else cfg.get("samples", 1)
     frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
                                  sun_radius=args.sun_radius if samples > 1 else 0.0)
     K = max(1, args.inflight)
 
-    gather_desc = mg = split_ms = None
+    X = Y = Z = 0
+    t_scene = 0.0
+    scene = noise = None
+    if not standin:
+        grid = presets.scene_grid(cfg["scene"])
+        Z, Y, X = grid.shape
+        noise = scenes.real_noise()            # the reference's res/noise.bin.gz (u_noise, render.js:138)
+        t_scene = time.perf_counter()
+        # palette grid in, distance field + octant copies built on the device (f-1);
+        # the noise texture through the product's .gz loader
+        scene = vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_path=scenes.NOISE_PATH,
+                         dims=(X, Y, Z), device=local)
+        t_scene = time.perf_counter() - t_scene
+        del grid
+
+    shards = None
     if world == 1:
         r = single_gpu(torch, vx, scene, frame, W, H, K, args.steps, args.warmup, args.settle_ms)
         stats, wall, settle_steps, ev_ms = r["stats"], r["wall_s"], r["settle"], r["ev_ms"]
     else:
-        streams = [torch.cuda.Stream() for _ in range(K)]
-        torch.cuda.set_stream(streams[0])
-        frames = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(K)]
-        group = None
-        if args.gather == "native":
-            uid = [vx.mgpu_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            try:
-                mg = vx.MultiGPU(scene, uid[0], world, rank)
-                ok = torch.tensor([1])
-            except Exception as e:          # RCCL init refused: fall back to the torch-driven gather
-                print(f"rank {rank}: vx_mgpu_create failed ({e}); falling back to --gather torch", file=sys.stderr)
-                mg, ok = None, torch.tensor([0])
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if int(ok.item()) == 0:
-                if mg is not None:
-                    mg.close()
-                    mg = None
-                args.gather = "torch-fallback"
-                group = dist.new_group(list(range(world)), backend="nccl")
-        if args.gather == "native":
-            fns = [(lambda fb=frames[j], sj=streams[j].cuda_stream:
-                    mg.render(frame, BAND, fb.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sj)) for j in range(K)]
-            st = mg.render(frame, BAND, frames[0].data_ptr(), pixel_format=vx.PIXEL_RGBA8,
-                           stream=streams[0].cuda_stream, stats=True)
-            gather_desc = "vx_mgpu_render: one RCCL ncclSend/ncclRecv group into rank 0's frame rows (native C++)"
-        else:
-            from voxmap_amd.dist import BandGather
-            gs = []
-            for j in range(K):
-                sj = streams[j].cuda_stream
-                g = BandGather(dist, W, H, BAND, 4, torch.uint8, "cuda",
-                               lambda ids, fr, sj=sj: scene.render_bands(frame, BAND, ids, fr.data_ptr(),
-                                                                         inplace=True, stream=sj), group=group)
-                g.frame = frames[j]
-                gs.append(g)
-
-            def mk(j):
-                def f():
-                    with torch.cuda.stream(streams[j]):
-                        gs[j].step()
-                return f
-            fns = [mk(j) for j in range(K)]
-            st = scene.render_bands(frame, BAND, gs[0].mine, frames[0].data_ptr(), inplace=True,
-                                    stream=streams[0].cuda_stream, stats=True)
-            gather_desc = ("torch.distributed batch_isend_irecv (RCCL) into rank 0's frame rows" +
-                           (" (fallback: vx_mgpu_create failed)" if group is not None else ""))
-        keys = [k for k in st.as_dict().keys() if k != "kernel_ms"]
-        vec = torch.tensor([float(st.as_dict()[k]) for k in keys], dtype=torch.float64)
-        if args.gather == "torch":
-            vec = vec.cuda()
-        dist.all_reduce(vec)
-        stats = {k: float(v) for k, v in zip(keys, vec.cpu().tolist())}
-        stats["kernel_ms"] = float(st.kernel_ms)
-        n = [0]
-
-        def step():
-            fns[n[0] % K]()
-            n[0] += 1
-        wall, settle_steps = timed(torch, step, args.steps, args.warmup, args.settle_ms, dist)
+        stats, wall, settle_steps, shards = multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world,
+                                                       local, standin)
         ev_ms = None
-        tt = torch.tensor([wall], dtype=torch.float64)
-        if args.gather == "torch":
-            tt = tt.cuda()
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
-        if mg is not None:
-            # render and gather timed apart (one stream, one frame at a
-            # time, max over ranks): vx_render_bands of this rank's bands, then
-            # vx_mgpu_gather alone (collective)
-            try:
-                mine = vx.mgpu_bands(H, BAND, world, rank)
-                s0 = streams[0].cuda_stream
-
-                def r_only():
-                    if mine:
-                        scene.render_bands(frame, BAND, mine, frames[0].data_ptr(), inplace=True, stream=s0)
-
-                def g_only():
-                    mg.gather(W, H, BAND, frames[0].data_ptr(), stream=s0)
-                tr, _ = timed(torch, r_only, args.steps, 2, 0.0, dist)
-                tg, _ = timed(torch, g_only, args.steps, 2, 0.0, dist)
-                t2 = torch.tensor([tr, tg], dtype=torch.float64)
-                dist.all_reduce(t2, op=dist.ReduceOp.MAX)
-                split_ms = {"render_ms": round(1000.0 * float(t2[0]) / args.steps, 4),
-                            "gather_ms": round(1000.0 * float(t2[1]) / args.steps, 4),
-                            "gather_bytes": int(W * 4 * sum(min(BAND, H - b * BAND)
-                                                            for b in range(-(-H // BAND)) if b % world)),
-                            "how": "one stream, one frame at a time, max over ranks (the timed step overlaps "
-                                   "frames in flight, so it is less than the sum)"}
-            except Exception as e:            # never let the diagnostic break the bench line
-                split_ms = {"error": str(e)}
     ms_per_step = 1000.0 * wall / args.steps
 
-    v1 = c5 = None
+    v1 = c5 = d2h = None
     if world == 1 and flags != 0 and args.flags is None and samples <= 1:
         # the reference's own shader (v1, flags 0) on the same frame: the same
         # K-in-flight wall timing, and one stream with events for its roofline
@@ -315,8 +471,11 @@ def main():
         ms1w = 1000.0 * a["wall_s"] / args.steps
         v1 = {"ms_per_frame": round(ms1w, 4), "mrays_per_s": round(r1 / ms1w / 1e3, 3), "rays_per_frame": int(r1),
               "single_stream_ms_per_frame": round(a["ev_ms"], 4), "alg_bytes": int(s1["alg_bytes"]),
-              "roofline_frac": round(roofline_of(s1["alg_bytes"], a["ev_ms"])[1], 4)}
-    if world == 1 and args.config == "C3" and not args.no_c5 and args.flags is None and args.samples is None:
+              "roofline_frac": round(roofline_of(s1["alg_bytes"], a["ev_ms"])[1], 4),
+              "lane_util": lane_utils(s1)}
+    if world == 1 and not args.no_d2h:
+        d2h = fps_with_d2h(torch, vx, scene, frame, W, H, max(20, args.steps // 2))
+    if world == 1 and cfg_name == "C3" and not args.no_c5 and args.flags is None and args.samples is None:
         # BASELINE configs[4] in the same run (C5 next to C3)
         c5cfg = presets.CONFIGS["C5"]
         g5 = presets.scene_grid(c5cfg["scene"])
@@ -334,14 +493,14 @@ def main():
         rays5 = s5["pixels"] + s5["shadow_rays"] + s5["reflect_rays"]
         ms5 = 1000.0 * b["wall_s"] / n5
         ach5, frac5 = roofline_of(s5["alg_bytes"], b["ev_ms"])
-        t5j = pmc_entry("traffic_r02_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
+        t5j = pmc_entry("traffic_r03_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
         c5 = {"workload": f"C5: {c5cfg['w']}x{c5cfg['h']}, field {X5}x{Y5}x{Z5} (S-proc 3x nearest upsample), "
                           f"full quality + {c5cfg['samples']}-sample soft shadows (sun radius {args.sun_radius})",
               "ms_per_frame": round(ms5, 4), "mrays_per_s": round(rays5 / ms5 / 1e3, 3), "fps": round(1000 / ms5, 2),
               "rays_per_frame": int(rays5), "single_stream_ms_per_frame": round(b["ev_ms"], 4),
               "alg_bytes": int(s5["alg_bytes"]), "roofline_achieved_gbps": round(ach5, 2),
               "roofline_frac": round(frac5, 4), "traffic": t5j.get("hbm_bytes_per_launch") if t5j else None,
-              "scene_build_s": round(t5, 3), "frames": n5}
+              "lane_util": lane_utils(s5), "scene_build_s": round(t5, 3), "frames": n5}
         sc5.close()
 
     rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
@@ -350,23 +509,23 @@ def main():
     if rank == 0:
         per_launch_bytes = float(stats["alg_bytes"]) / world if world > 1 else float(stats["alg_bytes"])
         kernel_ms = ev_ms if world == 1 else stats["kernel_ms"]
-        achieved, frac = roofline_of(per_launch_bytes, kernel_ms)
-        tag = "r02" if args.config != "C5" else "r02_c5"
-        traffic = pmc_entry(f"traffic_{tag}.json", args.config, cam, flags, samples) if world == 1 else None
-        valu = pmc_entry(f"valu_{tag}.json", args.config, cam, flags, samples) if world == 1 else None
-        if valu is None:
+        achieved, frac = roofline_of(per_launch_bytes, kernel_ms) if kernel_ms else (0.0, 0.0)
+        tag = "r03" if cfg_name != "C5" else "r03_c5"
+        traffic = pmc_entry(f"traffic_{tag}.json", cfg_name, cam, flags, samples) if world == 1 else None
+        valu = pmc_entry(f"valu_{tag}.json", cfg_name, cam, flags, samples) if world == 1 else None
+        if valu is None and not standin:
             # the same kernel instantiation measured on another workload (C2/C4 and
             # every rank of N > 1 run the C3 kernel; soft shadows the C5 one)
             ref_cfg = "C5" if samples > 1 else "C3"
             c_ref = presets.CONFIGS[ref_cfg]
-            valu = pmc_entry(f"valu_r02{'_c5' if samples > 1 else ''}.json", ref_cfg, c_ref["camera"], flags,
+            valu = pmc_entry(f"valu_r03{'_c5' if samples > 1 else ''}.json", ref_cfg, c_ref["camera"], flags,
                              c_ref.get("samples", 1) if samples > 1 else 1)
             if valu is not None:
                 valu = dict(valu, source=f"{valu.get('source', '')}; measured on {ref_cfg}, the same kernel "
-                                         f"instantiation as this {args.config} run")
+                                         f"instantiation as this {cfg_name} run")
         result = {
             "metric": f"Mrays/s at {cfg['w']}x{cfg['h']} {'full quality' if flags else 'v1 shading'} "
-                      f"({args.config}); fps; % HBM roofline",
+                      f"({cfg_name}); fps; % HBM roofline",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -377,36 +536,42 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": f"synthetic {cfg['scene']} field (seed 1) in map.bin layout (the real map.blob is "
-                    "AES-encrypted, key not in the repo); the reference's own res/noise.bin.gz noise texture",
+            "data": ("stand-in CPU band renderer (orchestration test, no GPU)" if standin else
+                     f"synthetic {cfg['scene']} field (seed 1) in map.bin layout (the real map.blob is "
+                     "AES-encrypted, key not in the repo); the reference's own res/noise.bin.gz noise texture"),
             "config": {
-                "workload": f"{args.config}: {W}x{H} frame, " + (
+                "workload": f"{cfg_name}: {W}x{H} frame, " + (
                     "full quality = v1 shading (primary visibility + sun march + trilinear AO + sky/clouds + glass) "
                     "+ ext reflection + rough normals" if flags == vx.FLAG_FULL_QUALITY else
                     f"v1 shading flags={flags}") +
                     (f" + {samples}-sample soft shadows (sun radius {args.sun_radius})" if samples > 1 else "") +
                     f", field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, RGBA8 framebuffer in HBM",
+                "value_is": (f"rays marched per second over {K} frames in flight ({K} streams, {K} framebuffers), "
+                             "inputs and framebuffers HBM-resident; the roofline uses the one-stream launch time"
+                             if world == 1 else
+                             f"rays marched per second by all {world} ranks, the RCCL gather to rank 0 inside "
+                             f"each step, {K} frames in flight"),
                 "flags": flags, "shadow_samples": samples, "scene_build_s": round(t_scene, 3),
                 "clock_settle": {"ms": args.settle_ms, "untimed_frames": settle_steps},
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
-                "shards": ({"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
-                            "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc,
-                            "split_ms": split_ms}
-                           if world > 1 else None),
+                "shards": shards,
                 "fps": round(1000.0 / ms_per_step, 2),
+                "fps_with_d2h": d2h,
                 "inflight": {"frames": K, "streams": K, "framebuffers": K,
                              "single_stream_ms_per_frame": round(ev_ms, 4) if ev_ms is not None else None},
                 "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
                 "shadow_rays": int(stats["shadow_rays"]), "reflect_rays": int(stats["reflect_rays"]),
+                "lane_util": lane_utils(stats) if world == 1 else None,
                 "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / wall / 1e6, 3),
                 "v1": v1,
                 "c5": c5,
             },
             "roofline": {
                 # achieved/peak/frac: the contract's unit, algorithmic bytes
-                # over the HBM peak.  "bound" is the resource that measurably binds the
-                # kernel: VALU issue (valu block: rocprofv3 PMC kept under profiles/), the
-                # field being cache-resident (traffic = fabric bytes << algorithmic)
+                # over the HBM peak, per launch on ONE stream.  "bound" is the resource
+                # that measurably binds the kernel: VALU issue (valu block: rocprofv3 PMC
+                # kept under profiles/), the field being cache-resident (traffic = fabric
+                # bytes << algorithmic)
                 "bound": "valu" if valu else "hbm",
                 "kernel": "k_render (fused primary visibility + shading + sun march" +
                           (" + reflection walk" if flags & vx.FLAG_REFLECT else "") + ")",
@@ -416,23 +581,25 @@ def main():
                 "frac": round(frac, 4),
                 "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
                 "alg_bytes_per_launch": int(per_launch_bytes),
-                "avg_launch_ms": round(kernel_ms, 4),
+                "avg_launch_ms": round(kernel_ms, 4) if kernel_ms else None,
                 "fabric_gbps": (round(traffic["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 1)
                                 if traffic else None),
                 "valu": ({k: valu[k] for k in ("valu_busy", "valu_lane_util", "valu_insts_per_wave", "clock_ghz",
                                                "source") if k in valu} if valu else None),
             },
         }
+        if standin:
+            result["config"]["standin_frame_ok"] = stats.get("standin_frame_ok")
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(scene, noise, frame, W, H, args.cpu_seconds)
-    if mg is not None:
-        mg.close()
-    scene.close()
+    if scene is not None:
+        scene.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+    return 0
 
 
 def host_cores():
@@ -508,4 +675,4 @@ def cpu_baseline(scene, noise, frame, W, H, target_s):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 5
+#define VX_ABI_VERSION 6
 
 /* error codes */
 #define VX_OK 0
@@ -146,7 +146,11 @@ typedef struct vx_stats {
     uint64_t reflect_rays, reflect_fetches;   /* ext REFLECT: reflection rays traced, texels read */
     uint64_t rough_px;          /* ext ROUGH: fragments with a jittered normal (4 noise texels each) */
     uint64_t primary_wave_iters, march_wave_iters;   /* diagnostic: loop iterations summed over
-                                   waves; lane utilisation = fetches / (64 * wave_iters) */
+                                   waves (the primary's entry fetch counts as one); lane
+                                   utilisation = fetches / (64 * wave_iters) <= 1 */
+    uint64_t march_lane_slots;  /* diagnostic (ABI 6): per march wave iteration, the lanes that
+                                   began that march; shadow_fetches / march_lane_slots = the
+                                   utilisation of the marching lanes alone */
     uint64_t alg_bytes;         /* 4*(primary+shadow+reflect fetches) + 32*ao + 80*clouded sky
                                    + 16*rough + out bytes */
     double kernel_ms;           /* HIP-event time of the render kernel(s) */
@@ -212,7 +216,9 @@ int vx_render_bands(vx_scene *scene, const vx_frame_params *p, int w, int h, int
  * rank b % nranks, vx_mgpu_bands), renders each rank's bands in place into its
  * own w*h frame_device and gathers them into rank 0's frame_device with one
  * RCCL group of ncclSend/ncclRecv: rank 0's frame is the finished image, no
- * de-tile pass.  stats: this rank's bands only. */
+ * de-tile pass.  stats: this rank's bands only.  stream NULL: the scene's own
+ * stream, for the render and the gather alike (the gather never reads rows a
+ * render on another stream has not finished). */
 #define VX_MGPU_UID_BYTES 128
 typedef struct vx_mgpu vx_mgpu;
 int vx_mgpu_unique_id(void *uid_out);
@@ -228,6 +234,20 @@ int vx_mgpu_rank(const vx_mgpu *m, int *nranks, int *rank);
 void vx_mgpu_destroy(vx_mgpu *m);
 /* The deal: the band ids of `rank` (ascending) into ids[0..cap); returns their count. */
 int vx_mgpu_bands(int h, int band_rows, int nranks, int rank, int *ids, int cap);
+/* One point-to-point move of the gather (ABI 6): band `band` (rows
+ * [band*band_rows, band*band_rows + rows)) goes from rank `src` (its owner) to
+ * rank `dst` = 0; the bytes lie at `offset` of the w x h frame on both ranks. */
+typedef struct vx_mgpu_xfer {
+    int band, src, dst, rows;
+    uint64_t offset, bytes;
+} vx_mgpu_xfer;
+/* The gather's transfer list as `rank` issues it (a pure host function, no
+ * GPU): rank 0 receives every band whose owner is not 0, rank r > 0 sends its
+ * own bands, in ascending band order.  Writes up to cap entries (out may be
+ * NULL) and returns the count.  vx_mgpu_gather issues exactly these, as
+ * ncclRecv (rank 0) / ncclSend (the owner) inside one RCCL group. */
+int vx_mgpu_transfers(int w, int h, int band_rows, int pixel_format, int nranks, int rank, vx_mgpu_xfer *out,
+                      int cap);
 
 /* --- host helpers (map.js / math.js / sdf.cpp / utils.js) ----------------- */
 /* map.js:373-391 orbit camera + math.js:37-42 projection (with its sqrt(aspect)

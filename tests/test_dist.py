@@ -106,3 +106,36 @@ def test_band_deal_is_a_partition_and_matches_native(built):
             assert max(sizes) - min(sizes) <= 1                      # balanced to one band
             for r in range(world):
                 assert vx.mgpu_bands(h, br, world, r) == lists[r]    # the native deal (vx_mgpu_bands)
+
+
+@pytest.mark.parametrize("fmt,px", [(1, 4), (0, 16)])
+def test_gather_schedule_native_matches_mirror(built, fmt, px):
+    """vx_mgpu_transfers (what vx_mgpu_gather issues as one RCCL group) equals the
+    mirror's schedule for N = 1..8, ragged last bands and both pixel formats; every
+    send has its matching receive on rank 0, and rank 0's own bands plus what it
+    receives tile the frame exactly once."""
+    import voxmap_amd as vx
+    from voxmap_amd.dist import bands, transfers
+    for w, h, br in ((7680, 4320, 64), (3840, 2160, 64), (100, 70, 8), (64, 8, 8), (4096, 6112, 64), (33, 1000, 24)):
+        for world in range(1, 9):
+            sched = [vx.mgpu_transfers(w, h, br, world, r, fmt) for r in range(world)]
+            for r in range(world):
+                assert sched[r] == transfers(w, h, br, world, r, px), (w, h, br, world, r)
+            recv = sched[0]
+            sends = sorted(x for r in range(1, world) for x in sched[r])
+            assert sends == recv                                       # one matching send per receive
+            assert all(x[1] == x[0] % world and x[2] == 0 for x in recv)
+            covered = np.zeros(h, np.int32)
+            for b in bands(h, br, world, 0):
+                covered[b * br:min(h, (b + 1) * br)] += 1
+            for b, src, dst, rows, off, nbytes in recv:
+                assert off == b * br * w * px and nbytes == rows * w * px
+                covered[off // (w * px):off // (w * px) + rows] += 1
+            assert (covered == 1).all(), (w, h, br, world)
+
+
+def test_gather_schedule_rejects_bad_arguments(built):
+    import voxmap_amd as vx
+    for args in ((0, 8, 8, 2, 0, 1), (8, 8, 8, 2, 2, 1), (8, 8, 0, 2, 0, 1), (8, 8, 8, 2, 0, 7)):
+        with pytest.raises(vx.VoxmapError):
+            vx.mgpu_transfers(*args[:5], pixel_format=args[5])

@@ -9,7 +9,7 @@ from ._abi import (FLAG_FULL_QUALITY, FLAG_INT_INDEX, FLAG_SOFT_POOL, FLAG_SOFT_
                    FLAG_ROUGH, FORMAT_AUTO, FORMAT_BIN, FORMAT_BIN_GZ, FORMAT_BLOB, FORMAT_GRID, PIXEL_RGBA8, PIXEL_RGBA32F,
                    FrameParams, Stats, VoxmapError, lib)
 from .renderer import (Frame, MultiGPU, Scene, blob_encrypt, decode, field_build, frame_from_matrix, frame_from_orbit,
-                       hour_from_time_ms, make_frame, mgpu_bands, mgpu_unique_id, noise_synth, field_build_gpu,
+                       hour_from_time_ms, make_frame, mgpu_bands, mgpu_transfers, mgpu_unique_id, noise_synth, field_build_gpu,
                        params_to_dict, sun_from_hour, sun_samples, vertex2d)
 
 __all__ = [
@@ -18,5 +18,5 @@ __all__ = [
     "blob_encrypt", "params_to_dict", "PIXEL_RGBA32F", "PIXEL_RGBA8", "FORMAT_AUTO", "FORMAT_BIN",
     "FORMAT_BIN_GZ", "FORMAT_BLOB", "FLAG_NO_SHADOW", "FLAG_NO_AO", "FLAG_NO_CLOUDS", "FLAG_PRIMARY_ONLY",
     "FLAG_REFLECT", "FLAG_ROUGH", "FLAG_FULL_QUALITY", "FLAG_INT_INDEX", "FLAG_SOFT_POOL", "FLAG_SOFT_BRICK", "sun_samples", "field_build_gpu", "FORMAT_GRID",
-    "MultiGPU", "mgpu_unique_id", "mgpu_bands", "vertex2d",
+    "MultiGPU", "mgpu_unique_id", "mgpu_bands", "mgpu_transfers", "vertex2d",
 ]

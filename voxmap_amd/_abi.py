@@ -30,7 +30,7 @@ FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary i
 FLAG_SOFT_POOL = 0x80                           # soft shadows by the pooled wave march (same frames)
 FLAG_SOFT_BRICK = 0x100                         # + LDS 8^3 brick staging (same frames)
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 5
+ABI_VERSION = 6
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128
 
@@ -62,13 +62,19 @@ class FrameParams(C.Structure):
         return out
 
 
+class MgpuXfer(C.Structure):
+    """vx_mgpu_xfer: one band moved by the gather."""
+    _fields_ = [("band", C.c_int), ("src", C.c_int), ("dst", C.c_int), ("rows", C.c_int),
+                ("offset", C.c_uint64), ("bytes", C.c_uint64)]
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("pixels", C.c_uint64), ("sky_px", C.c_uint64), ("block_px", C.c_uint64), ("glass_px", C.c_uint64),
         ("primary_fetches", C.c_uint64), ("shadow_rays", C.c_uint64), ("shadow_fetches", C.c_uint64),
         ("ao_samples", C.c_uint64), ("noise_px", C.c_uint64), ("primary_cap_hits", C.c_uint64),
         ("reflect_rays", C.c_uint64), ("reflect_fetches", C.c_uint64), ("rough_px", C.c_uint64),
-        ("primary_wave_iters", C.c_uint64), ("march_wave_iters", C.c_uint64),
+        ("primary_wave_iters", C.c_uint64), ("march_wave_iters", C.c_uint64), ("march_lane_slots", C.c_uint64),
         ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double),
     ]
 
@@ -103,6 +109,7 @@ SIGNATURES = [
     ("vx_mgpu_rank", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("vx_mgpu_destroy", None, [C.c_void_p]),
     ("vx_mgpu_bands", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int]),
+    ("vx_mgpu_transfers", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
     ("vx_frame_from_orbit", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
                                       C.POINTER(FrameParams)]),
     ("vx_frame_from_matrix", C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(FrameParams)]),

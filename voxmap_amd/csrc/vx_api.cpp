@@ -19,10 +19,6 @@
 
 #include "vx_internal.h"
 
-#ifndef VX_SUN_BRICK
-#define VX_SUN_BRICK 0
-#endif
-
 namespace vx {
 int decode_container(const unsigned char *in, size_t n, int format, const char *key,
                      std::vector<unsigned char> &out, size_t expect);
@@ -74,6 +70,7 @@ struct vx_scene {
     } while (0)
 
 int vx::scene_device(const vx_scene *s) { return s->device; }
+void *vx::scene_stream(const vx_scene *s) { return (void *)s->stream; }
 
 static int read_file(const char *path, std::vector<unsigned char> &buf) {
     std::ifstream f(path, std::ios::binary);
@@ -253,12 +250,9 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         const size_t sxy = (size_t)(X + 2 * (Z + 2)) * (Y + 2 * (Z + 2));
         // the march's byte offset is 0x4B000000 + x + Xp*y + XpYp*z from fp32 bit patterns
         // (vx_kernels.hip march_pad): the padded plane below 2^23, the sum below 2^32
-        if (!lrc && Z <= 126 && max_rg <= Z && sxy < (1u << 23) && sxy * (Z + 2 * (Z + 2) + 3) + (VX_SUN_BRICK ? 0ull : 1ull) * 0x4B000000u < (1ull << 32)) {
+        if (!lrc && Z <= 126 && max_rg <= Z && sxy < (1u << 23) && sxy * (Z + 2 * (Z + 2) + 3) + 0x4B000000ull < (1ull << 32)) {
             s->SB = Z + 2;
             s->SXp = X + 2 * s->SB; s->SYp = Y + 2 * s->SB; s->SZp = Z + 2 * s->SB;
-#if VX_SUN_BRICK
-            s->SXp = (s->SXp + 7) & ~7; s->SYp = (s->SYp + 3) & ~3; s->SZp = (s->SZp + 3) & ~3;   // whole bricks
-#endif
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
             if ((e = hipMalloc(&s->d_sunp, 2 * np)) == hipSuccess &&
                 (e = hipMemsetAsync(s->d_sunp, 0xFF, 2 * np, s->stream)) == hipSuccess)
@@ -377,6 +371,7 @@ static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int 
     st->rough_px = v[ST_ROUGH];
     st->primary_wave_iters = v[ST_PRIM_WITERS];
     st->march_wave_iters = v[ST_MARCH_WITERS];
+    st->march_lane_slots = v[ST_MARCH_SLOTS];
     // 4 B per field texel read (primary, shadow and reflection
     // rays), 32 B per trilinear AO, 80 B per clouded sky pixel (5 bilinear
     // noise taps), 16 B per rough-normal white() tap (4 texels), plus the
@@ -405,13 +400,8 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.sun = s->d_sun;
     a.sunp = s->d_sunp;
     a.SB = s->SB;
-#if VX_SUN_BRICK
-    a.SXp = 4 * (s->SXp >> 3) - 1;                                        // 4 NBX - 1 (march_pad)
-    a.SXpYp = (unsigned)(s->SXp >> 3) * (unsigned)(s->SYp >> 2) - 1u;     // NBXY - 1
-#else
     a.SXp = s->SXp;
     a.SXpYp = (unsigned)s->SXp * (unsigned)s->SYp;
-#endif
     a.sunp_texels = (unsigned)s->SXp * (unsigned)s->SYp * (unsigned)s->SZp;
     a.rg = s->d_rg;
     a.noise = s->d_noise;

@@ -13,6 +13,8 @@ namespace vx {
 int set_error(int code, const std::string &msg);
 // the HIP device ordinal a scene lives on (vx_api.cpp)
 int scene_device(const vx_scene *s);
+// the scene's own (non-blocking) stream: what vx_render* run on when given stream == NULL
+void *scene_stream(const vx_scene *s);
 
 // One sun direction of the march (render.frag:75-142) with the per-frame
 // constants its loop needs: sign(r), |r|, RN(1/|r|) (Markstein division).
@@ -102,7 +104,8 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
 
 enum StatSlot {
     ST_PIXELS = 0, ST_SKY, ST_BLOCK, ST_GLASS, ST_PRIM_FETCH, ST_SHADOW_RAYS, ST_SHADOW_FETCH,
-    ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_REFL_RAYS, ST_REFL_FETCH, ST_ROUGH, ST_PRIM_WITERS, ST_MARCH_WITERS, ST_COUNT
+    ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_REFL_RAYS, ST_REFL_FETCH, ST_ROUGH, ST_PRIM_WITERS, ST_MARCH_WITERS,
+    ST_MARCH_SLOTS, ST_COUNT
 };
 
 // Field data in HBM (vx_kernels.hip): `prim` = 8 copies (one

@@ -4,71 +4,26 @@
 // rasterising vertex.bin) -> render.frag main() shading with
 // the sun march() (render.frag:75-142) -> glass blend -> framebuffer store.
 // Lane = pixel; a wave64 covers an 8x8 pixel tile, a 256-thread workgroup a
-// 16x16 tile, so the rays of a wave march through neighbouring cells.
+// 32x8 block, so the rays of a wave march through neighbouring cells.
 //
 // Numerical contract: fp32, IEEE div/sqrt, no FMA contraction
 // (built with -ffp-contract=off), GLSL built-ins spelled out, vexp2 below, so
 // every pixel matches the scalar oracle (oracle/vxo_render.c) bit for bit.
 // Exactness-preserving rewrites used here (each justified in DESIGN.md §5):
-//   * a / b with b a per-frame constant -> two Markstein corrections from
+//   * a / b with b a per-frame constant -> one Markstein correction from
 //     y = RN(1/b) computed on the host (exhaustively checked:
-//     tools/markstein_check.c);
+//     tools/micro/markstein_all.hip);
 //   * length(m*t) with a single selected axis -> t (sqrt(RN(t*t)) == t);
-//   * unorm8 decode b/255 -> a 256-entry LDS table of the IEEE quotients;
+//   * unorm8 decode b/255 -> typed UNORM buffer loads (the texture data unit
+//     returns RN(b/255) for every byte, tools/micro/unorm_check.hip);
 //   * per-frame uniform-only expressions -> host (vx_frame.cpp).
+// Rejected experiments (bricked layouts, LDS r*k tables, hand-batched sky
+// loads, typed primary loads, ...) are measured in profiles/ and kept in git
+// history, not here.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
-
 #include "vx_internal.h"
-
-// Diagnostic padding (A/B only, never in the product build): VX_PAD_MARCH /
-// VX_PAD_PRIM extra independent v_add_f32 per loop iteration.
-// VX_RSTEP: the hard shadow's r*safe from a per-frame LDS table (round 1); off
-// since the typed SSCALED texel load (three multiplies on the loaded float are
-// off the LDS latency): C3 v1 -0.2 %, full quality -0.4 %.
-#ifndef VX_RSTEP
-#define VX_RSTEP 0
-#endif
-#ifndef VX_STOP_VGPR
-#define VX_STOP_VGPR 1
-#endif
-#ifndef VX_MARCH_PAD
-#define VX_MARCH_PAD 1
-#endif
-#ifndef VX_MARCH_SG
-#define VX_MARCH_SG 1
-#endif
-#ifndef VX_AO_CVT
-#define VX_AO_CVT 1
-#endif
-#ifndef VX_WRAP_FAST
-#define VX_WRAP_FAST 1
-#endif
-#ifndef VX_AO_DELTA
-#define VX_AO_DELTA 1
-#endif
-#ifndef VX_SUN_BRICK
-#define VX_SUN_BRICK 0
-#endif
-#if VX_SUN_BRICK
-#define VX_BRICK_CY cy
-#define VX_BRICK_CZ cz
-#define VX_BRICK_UNBIAS unbias
-#else
-#define VX_BRICK_CY 0u
-#define VX_BRICK_CZ 0u
-#define VX_BRICK_UNBIAS 0u
-#endif
-#ifndef VX_PAD_MARCH
-#define VX_PAD_MARCH 0
-#endif
-#ifndef VX_PAD_PRIM
-#define VX_PAD_PRIM 0
-#endif
-#define VX_PAD(N, ACC)                                                        \
-    _Pragma("unroll") for (int pad_i = 0; pad_i < (N); pad_i++) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(ACC));
 
 namespace vx {
 namespace {
@@ -94,17 +49,12 @@ __device__ __forceinline__ int f2i(float x) {
 // correction q1 = RN(q0 + fma(-q0, b, a)*y) is already correctly rounded
 // (Markstein's theorem for y = RN(1/b); tools/markstein_check.c: 0 mismatches
 // over every numerator in [1e-4, 1.0002] for thousands of divisors, random
-// and adversarial mantissas).  VX_MARKSTEIN_STEPS=2 keeps a second one.
-#ifndef VX_MARKSTEIN_STEPS
-#define VX_MARKSTEIN_STEPS 1
-#endif
+// and adversarial mantissas; tools/micro/markstein_all.hip: every pair of
+// significands).
 __device__ __forceinline__ float div_const(float a, float b, float y) {
     const float q0 = a * y;
     const float r0 = __builtin_fmaf(-q0, b, a);
-    const float q1 = __builtin_fmaf(r0, y, q0);
-    if (VX_MARKSTEIN_STEPS < 2) return q1;
-    const float r1 = __builtin_fmaf(-q1, b, a);
-    return __builtin_fmaf(r1, y, q1);
+    return __builtin_fmaf(r0, y, q0);
 }
 
 // exp2 by the fixed degree-9 polynomial of the numerical contract.
@@ -165,26 +115,27 @@ struct Counters {
     unsigned prim_fetch, shadow_rays, shadow_fetch, ao, noise_px, cap_hit;
     unsigned refl_rays, refl_fetch, rough;   // extensions
     unsigned prim_witers, march_witers;      // loop iterations per wave (diagnostic: lane utilisation)
+    unsigned march_slots;                    // per march wave iteration: the lanes that began that march
 };
 
 // (float)((t >> 8k) & 0xff) as one v_cvt_f32_ubyteK (left to itself the
 // compiler may fold the mask away and emit a shift + convert)
-[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte0(uint32_t t) {
+__device__ __forceinline__ float cvt_f32_ubyte0(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
-[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
+__device__ __forceinline__ float cvt_f32_ubyte1(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
-[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte2(uint32_t t) {
+__device__ __forceinline__ float cvt_f32_ubyte2(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(t));
     return r;
 }
-[[maybe_unused]] __device__ __forceinline__ float cvt_f32_ubyte3(uint32_t t) {
+__device__ __forceinline__ float cvt_f32_ubyte3(uint32_t t) {
     float r;
     asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(t));
     return r;
@@ -195,6 +146,8 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
     const unsigned long long act = __ballot(1);
     return __lane_id() == (unsigned)(__ffsll((unsigned long long)act) - 1) ? v : 0u;
 }
+// the lanes of the wave that run this code (a march's marching lanes, taken at its start)
+__device__ __forceinline__ unsigned active_lanes() { return (unsigned)__popcll(__ballot(1)); }
 
 // Field data in HBM, each array shaped for the loop that
 // reads it, so a cache line holds as many useful cells as possible:
@@ -205,12 +158,13 @@ __device__ __forceinline__ unsigned once_per_wave(unsigned v) {
 //         (0xFFFFFFFF: colour 0xFF is no vis colour, extents are <= cap - 1 <=
 //         254), so the primary traversal detects leaving the grid from the value
 //         it loads;
-//   sun   map.bin's R ("up") and G ("down") channels, u8 each, linear: the
-//         sun march reads one of them;
+//   sunp  map.bin's R ("up") and G ("down") channels, int8 each, inside a
+//         border of -1 cells: the sun march reads one of them;
+//   sun   the same channels u8, unpadded (the literal march);
 //   rg    R | G << 8, u16, linear: the AO trilinear sample.
 // Every read is in bounds: the traversal stays within P of the grid, march()
 // returns before reading outside it, the AO sample clamps.
-[[maybe_unused]] constexpr uint32_t kSentinel = 0xFFFFFFFFu;   // border cells: colour 0xFF, extents 255
+constexpr uint32_t kSentinel = 0xFFFFFFFFu;   // border cells: colour 0xFF, extents 255
 
 // Loads at a 32-bit byte offset from a wave-uniform base: lets the compiler
 // use the saddr form (SGPR base + VGPR offset) instead of 64-bit per-lane
@@ -220,70 +174,22 @@ __device__ __forceinline__ T ld_off(const T *base, unsigned byte_off) {
     return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + byte_off);
 }
 
-// The march's texel load as an asm statement: its result is a plain 32-bit
-// value (the compiler keeps an i8 load's result in 16 bits across the loop's
-// back edge and sign-extends it again every step).  The compiler does not
-// track this load, so wait_vmem(v) must come before any use of v: an
-// s_waitcnt tied to v, placed where the compiler would have put its own.
-// f0..f2 pass through the statement untouched: what reads them (the next
-// step's length) is scheduled after the load, under its latency.
-__device__ __forceinline__ int ld_sbyte_async(const int8_t *base, unsigned byte_off, float &f0, float &f1, float &f2) {
-    int v;
-    asm volatile("global_load_sbyte %0, %4, %5" : "=&v"(v), "+v"(f0), "+v"(f1), "+v"(f2) : "v"(byte_off), "s"(base));
-    return v;
-}
-__device__ __forceinline__ void wait_vmem(int &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
-__device__ __forceinline__ void wait_vmem(float &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
-
-// VX_FMT_LOAD: the march texel through a typed buffer load whose descriptor
-// says "8-bit, SSCALED" (DATA_FORMAT 1, NUM_FORMAT 3, DST_SEL_X = X): the
-// texture data unit returns (float)(int8)texel, so the loop needs no
-// byte -> float convert.  The descriptor's base is the channel moved down by
-// the offset bias (0x4B000000, march_pad), num_records = 2^32 - 1 (offsets are
-// in bounds by the -1 border, as for the global load).
-#ifndef VX_FMT_LOAD
-#define VX_FMT_LOAD 1
-#endif
+// Typed buffer loads: the texture data unit converts the texel.
+//   * the march texel: descriptor "8-bit, SSCALED" (DATA_FORMAT 1, NUM_FORMAT
+//     3, DST_SEL_X = X) returns (float)(int8)texel, so the loop has no
+//     byte -> float convert; base = the channel moved down by the offset bias
+//     (0x4B000000, march_pad), num_records = 2^32 - 1 (offsets are in bounds
+//     by the -1 border);
+//   * AO and noise texels: NUM_FORMAT UNORM returns RN(b / 255) for every
+//     byte b, the exact render.frag:38 decode (tools/micro/unorm_check.hip: all
+//     256 bytes, 8, 8_8 and 8_8_8_8 formats, profiles/r02_unorm_check.txt).
+// All of them through the LLVM intrinsic: the compiler sees the loads, places
+// the waits, schedules independent work under them and never copies or spills
+// a register a load has not written yet.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 fmt_rsrc(const int8_t *base) {
-    const unsigned long long p = (unsigned long long)base;
-    u32x4 r;
-    r.x = __builtin_amdgcn_readfirstlane((unsigned)p);
-    r.y = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32) & 0xffffu);
-    r.z = 0xffffffffu;
-    r.w = 0x0000B004u;
-    return r;
-}
-__device__ __forceinline__ float ld_fmt_async(u32x4 rsrc, unsigned byte_off, float &f0, float &f1, float &f2) {
-    float v;
-    asm volatile("buffer_load_format_x %0, %4, %5, 0 offen" : "=&v"(v), "+v"(f0), "+v"(f1), "+v"(f2)
-                 : "v"(byte_off), "s"(rsrc));
-    return v;
-}
-// VX_TYPED_UNORM: texel channels decoded by the texture data unit.  A typed
-// buffer load with NUM_FORMAT UNORM returns RN(b / 255) for every byte b, the
-// exact render.frag:38 decode (tools/micro/unorm_check.hip: all 256 bytes, 8,
-// 8_8 and 8_8_8_8 formats, profiles/r02_unorm_check.txt), so the AO and noise
-// samples need no byte extraction and no LDS table read.
-#ifndef VX_TYPED_UNORM
-#define VX_TYPED_UNORM 1
-#endif
-// VX_PRIM_TYPED: the primary traversal's cell word through a typed USCALED
-// load (colour and extents as floats, no byte converts); parity-green and
-// measured +0.2..0.3 % on C3 (profiles/r02_ab_prim_typed_c3.txt): off.
-// VX_SKY_BATCH: the sky's four independent fbm loads placed first by hand; with
-// the compiler-visible typed loads its own schedule is better (C3 full -0.9 %
-// without it, profiles/r02_ab_unorm_intrinsics.txt): off
-#ifndef VX_SKY_BATCH
-#define VX_SKY_BATCH 0
-#endif
-#ifndef VX_PRIM_TYPED
-#define VX_PRIM_TYPED 0
-#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x3 __attribute__((ext_vector_type(3)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 unorm_rsrc(const void *base, unsigned w3) {
+__device__ __forceinline__ u32x4 buf_rsrc(const void *base, unsigned w3) {
     const unsigned long long p = (unsigned long long)base;
     u32x4 r;
     r.x = __builtin_amdgcn_readfirstlane((unsigned)p);
@@ -292,37 +198,25 @@ __device__ __forceinline__ u32x4 unorm_rsrc(const void *base, unsigned w3) {
     r.w = w3;
     return r;
 }
-#if VX_TYPED_UNORM
+constexpr unsigned kRsrcS8 = 0x0000B004u;  // 8, SSCALED, dst X: the march texel
 constexpr unsigned kRsrcRG = 0x1802Cu;     // 8_8, UNORM, dst (X, Y): (R, G) of a u16 R | G << 8
 constexpr unsigned kRsrcA = 0x50007u;      // 8_8_8_8, UNORM, dst X = W: the A channel
 constexpr unsigned kRsrcRGB = 0x501ACu;    // 8_8_8_8, UNORM, dst (X, Y, Z)
-// the LLVM typed-load intrinsics themselves: the compiler sees the loads, so it
-// places the waits, schedules them freely and never spills a register a load
-// has not written yet
 __device__ float vx_ld_format_f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.f32");
 __device__ f32x2 vx_ld_format_v2f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.v2f32");
 __device__ f32x3 vx_ld_format_v3f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.v3f32");
-__device__ __forceinline__ f32x2 ld_unorm2(u32x4 rsrc, unsigned off) { return vx_ld_format_v2f32(rsrc, off, 0, 0); }
-__device__ __forceinline__ float ld_unorm1(u32x4 rsrc, unsigned off) { return vx_ld_format_f32(rsrc, off, 0, 0); }
-__device__ __forceinline__ f32x3 ld_unorm3(u32x4 rsrc, unsigned off) { return vx_ld_format_v3f32(rsrc, off, 0, 0); }
-#endif
-__device__ __forceinline__ float ld_fmt(u32x4 rsrc, unsigned byte_off) {
-    float v;
-    asm("buffer_load_format_x %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(byte_off), "s"(rsrc));
-    return v;
-}
+__device__ __forceinline__ float ld_fmt1(u32x4 rsrc, unsigned off) { return vx_ld_format_f32(rsrc, off, 0, 0); }
+__device__ __forceinline__ f32x2 ld_fmt2(u32x4 rsrc, unsigned off) { return vx_ld_format_v2f32(rsrc, off, 0, 0); }
+__device__ __forceinline__ f32x3 ld_fmt3(u32x4 rsrc, unsigned off) { return vx_ld_format_v3f32(rsrc, off, 0, 0); }
 
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
 __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
     return (unsigned)x + __umul24((unsigned)a.X, (unsigned)y) + __umul24(a.XY, (unsigned)z);
 }
 
-// Buffer resource over a field array: loads take a 32-bit byte offset (no
-// 64-bit address arithmetic) and an offset past `bytes` reads 0 instead of
-// faulting.  Word 3 = 0x00020000: raw, untyped (gfx9 family).
 // ---------------- sun march: render.frag:75-142 ----------------
 // Fast exact path for sun directions with every |r_i| >= 2^-10 (no zero
 // component, so no 0*inf NaN; every t finite and < 1025).  `sun` is the
@@ -386,12 +280,6 @@ __device__ __forceinline__ float march_len_sg(const SunRay &S, float f0, float f
 //          is f_u itself or a multiple of ulp(1) = 2^-23.
 // The first step starts from the surface's fract, which can be slightly
 // negative (the hit point's rounding), so march_pad keeps march_len_sg there.
-#ifndef VX_FRACT
-#define VX_FRACT 1
-#endif
-#ifndef VX_EXY
-#define VX_EXY 1
-#endif
 template <int SG>
 __device__ __forceinline__ float march_len_fract(const SunRay &S, float f0, float f1, float f2) {
     const float d0 = __builtin_amdgcn_fractf((SG & 1) ? -f0 : f0) + 1e-4f;
@@ -409,7 +297,7 @@ __device__ __forceinline__ float march_len_fract(const SunRay &S, float f0, floa
 }
 
 __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
-                           float f1, float f2, unsigned &fetches, unsigned &witers) {
+                           float f1, float f2, Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
@@ -417,10 +305,9 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
     float safe = 1.0f;
     float e0 = (float)c0, e1 = (float)c1, e2 = (float)c2;
     float len = march_len(S, f0, f1, f2);
-    int step = 0;                                                                // wave-uniform
-    float pad_acc = 0.0f;
+    int step = 0;
+    const unsigned nl = active_lanes();
     do {
-        VX_PAD(VX_PAD_MARCH, pad_acc)
         f0 = f0 + (r0 * safe) * len;                                             // :118
         f1 = f1 + (r1 * safe) * len;
         f2 = f2 + (r2 * safe) * len;
@@ -430,15 +317,15 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
         const int i0 = (int)e0, i1 = (int)e1, i2 = (int)e2;
         const bool sky = (unsigned)i0 >= (unsigned)a.X || (unsigned)i1 >= (unsigned)a.Y || (unsigned)i2 >= (unsigned)a.Z;
         const uint32_t t = sun[sky ? 0u : lin_index(a, i0, i1, i2)];             // :123-128
-        fetches += sky ? 0u : 1u;
+        cnt.shadow_fetch += sky ? 0u : 1u;
+        cnt.march_witers += once_per_wave(1u);
+        cnt.march_slots += once_per_wave(nl);
         len = march_len(S, f0, f1, f2);                                          // next step, under the load
         // safe < 0 marks "lit": left the grid (:123-126), or the step that
         // reaches MAX_STEPS, whatever it read (:234 tests step, not safe)
         safe = sky ? -1.0f : (float)t;
         if (++step >= maxs) safe = -1.0f;
     } while (safe > 0.0f);
-    witers += once_per_wave((unsigned)step);
-    if (VX_PAD_MARCH) asm volatile("" ::"v"(pad_acc));
     return safe < 0.0f;
 }
 
@@ -446,129 +333,71 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
 // (vx_scene_create, Z <= 126): a step moves at most safe + 1 <= Z + 1 cells
 // per axis, so the texel a lane loads after leaving the grid is a border
 // cell and its -1 is the exit ("lit", render.frag:123-126) -- no bounds test.
-// Cells are padded-grid fp32 integers; the index x + Xp*y is one exact fp32
-// fma (< 2^24, checked on the host), then + XpYp*z in integers.  The last
-// step (step MAX_STEPS-1 -> MAX_STEPS) is lit whatever it reads (:234), so
-// the loop runs MAX_STEPS-1 steps with the step test on the scalar unit, and
-// a lane still marching afterwards is lit.
-// rstep (hard shadows): an LDS table of (r0*k, r1*k, r2*k) for k = 0..127, the
-// same fp32 products r*safe of :118 for every possible safe, indexed by the
-// loaded texel -- one ds_read_b128 instead of three multiplies and the
-// byte -> float convert.  nullptr: multiply in the loop (soft-shadow samples).
-template <int SG, bool TAB>   // SG -1: signs at run time; else the sun's axis signs (march_len_sg)
+// The last step (step MAX_STEPS-1 -> MAX_STEPS) is lit whatever it reads
+// (:234), so the loop runs MAX_STEPS-1 steps with the step test on the scalar
+// unit, and a lane still marching afterwards is lit.
+//
+// Cells as fp32 integers, x and z biased by 2^23 (exact below 2^24): the bit
+// pattern of 2^23 + n is 0x4B000000 + n, so the x + Xp*y part of the offset is
+// the bit pattern of one exact fma and the low 24 bits of the z pattern are z
+// itself -- no float -> int converts in the loop:
+//   bits(fma(y, Xp, 2^23 + x)) + u24(bits(2^23 + z)) * XpYp
+//     = 0x4B000000 + x + Xp*y + XpYp*z,
+// read from the channel base moved down by 0x4B000000 (vx_scene_create checks
+// Xp*Yp < 2^23 and the sum < 2^32).  The x + Xp*y part is carried as one
+// biased fp32 integer exy (2^23 <= exy < 2^24) and moved by fma(fl1, Xp, fl0)
+// per step.  The texel arrives as a float (kRsrcS8): safe directly, -1 = left
+// the grid.
+template <int SG>   // the sun's axis signs (bit i: r_i > 0)
 __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
-                                          int c2, float f0, float f1, float f2, unsigned &fetches, unsigned &witers,
-                                          const float4 *rstep) {
-    const FrameConsts &F = a.fc;
+                                          int c2, float f0, float f1, float f2, Counters &cnt) {
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
-    const int maxs = F.max_steps;
+    const int maxs = a.fc.max_steps;
     if (maxs <= 0) return maxs == 0;
     const float xpf = (float)a.SXp;
-    // Cells as fp32 integers, x and z biased by 2^23 (exact below 2^24): the
-    // bit pattern of 2^23 + n is 0x4B000000 + n, so the x + Xp*y part of the
-    // offset is the bit pattern of one exact fma and the low 24 bits of the z
-    // pattern are z itself -- no float -> int converts in the loop:
-    //   bits(fma(y, Xp, 2^23 + x)) + u24(bits(2^23 + z)) * XpYp
-    //     = 0x4B000000 + x + Xp*y + XpYp*z,
-    // read from the channel base moved down by 0x4B000000 (vx_scene_create
-    // checks Xp*Yp < 2^23 and the sum < 2^32).
     constexpr float kBias = 8388608.0f;
-#if VX_SUN_BRICK
-    // Bricked sunp (VX_SUN_BRICK): 8x4x4 cells per 128-B line, bricks x fastest.
-    // Cells carried as 2^23 + x, 2^23 + 8y, 2^23 + 32z; with X, Y8, Z32 their
-    // patterns' low 24 bits the offset is
-    //   X + 15 (X & ~7) + Y8 + (4 NBX - 1)(Y8 & ~31) + Z32 + (NBXY - 1)(Z32 & ~127)
-    //   = 128 brick + 32 (z & 3) + 8 (y & 3) + (x & 7)   (+ 3 * 0x4B000000)
-    float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(8 * (c1 + a.SB)) + kBias;
-    float e2 = (float)(32 * (c2 + a.SB)) + kBias;
-    const int8_t *sunb = sun;
-    const unsigned unbias = 0u - 3u * 0x4B000000u;   // the three patterns' exponent bits, mod 2^32
-    const unsigned cy = (unsigned)a.SXp, cz = a.SXpYp;
-#else
-    float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB) + kBias;
-    const int8_t *sunb = sun - 0x4B000000;   // (pointer arithmetic: keeps the global address space)
-#endif
-    // VX_EXY: the x + Xp*y part carried as one biased fp32 integer exy (exact:
-    // 2^23 <= exy < 2^24) and moved by fma(fl1, Xp, fl0) per step -- one add
-    // fewer than moving e0 and e1 and recombining them.
-    float exy = __builtin_fmaf(e1, xpf, e0);
-    float len = (SG < 0 ? march_len(S, f0, f1, f2) : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2));
+    float exy = __builtin_fmaf((float)(c1 + a.SB), xpf, (float)(c0 + a.SB) + kBias);
+    float e2 = (float)(c2 + a.SB) + kBias;
     const unsigned sxpyp = a.SXpYp;
-    // kFmt: the texel arrives as a float (VX_FMT_LOAD, soft-shadow samples)
-    constexpr bool kFmt = VX_FMT_LOAD && !TAB && !VX_SUN_BRICK;
-    typedef typename std::conditional<kFmt, float, int>::type texel_t;
-    const u32x4 rsrc = fmt_rsrc(sunb);
-    texel_t tv = 1;                            // texel of the current cell = safe (render.frag:86: 1)
-    // one step of :94-128 -> the texel (-1: left the grid)
-#define VX_PAD_STEP(T, ASYNC)                                                                 \
-    {                                                                                         \
-        float m0, m1, m2;                                                                     \
-        if constexpr (TAB) {                                                                  \
-            const float4 q = rstep[(int)tv];                                                  \
-            m0 = q.x; m1 = q.y; m2 = q.z;                                                     \
-        } else {                                                                              \
-            const float safe = kFmt ? (float)tv : cvt_f32_ubyte0((uint32_t)tv); /* 1..126 */  \
-            m0 = r0 * safe; m1 = r1 * safe; m2 = r2 * safe;                                   \
-        }                                                                                     \
-        f0 = f0 + m0 * len; /* :118 */                                                        \
-        f1 = f1 + m1 * len;                                                                   \
-        f2 = f2 + m2 * len;                                                                   \
-        const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);                     \
-        f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2; /* :120 */                               \
-        unsigned off;                                                                         \
-        if (VX_SUN_BRICK) {                                                                   \
-            e0 += fl0; /* :119 (exact), y and z scaled */                                     \
-            e1 = __builtin_fmaf(fl1, 8.0f, e1);                                               \
-            e2 = __builtin_fmaf(fl2, 32.0f, e2);                                              \
-            const unsigned bx = __float_as_uint(e0), by = __float_as_uint(e1);               \
-            const unsigned bz = __float_as_uint(e2);                                          \
-            off = __umul24(bx & ~7u, 15u) + bx + __umul24(by & ~31u, VX_BRICK_CY) + by +      \
-                  __umul24(bz & ~127u, VX_BRICK_CZ) + bz + VX_BRICK_UNBIAS;                   \
-        } else if (VX_EXY) {                                                                  \
-            exy += __builtin_fmaf(fl1, xpf, fl0); e2 += fl2; /* :119 (exact) */               \
-            off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy);                \
-        } else {                                                                              \
-            e0 += fl0; e1 += fl1; e2 += fl2; /* :119 (exact) */                               \
-            off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(__builtin_fmaf(e1, xpf, e0)); \
-        }                                                                                     \
-        if constexpr (kFmt)                                                                   \
-            T = ASYNC ? ld_fmt_async(rsrc, off, f0, f1, f2) : ld_fmt(rsrc, off);             \
-        else                                                                                  \
-            T = ASYNC ? ld_sbyte_async(sunb, off, f0, f1, f2) /* :123-128, wait_vmem before use */ \
-                      : (int)ld_off(sunb, off);                                               \
-    }
+    const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);   // (pointer arithmetic: keeps the global address space)
+    float len = march_len_sg<SG>(S, f0, f1, f2);
+    float tv = 1.0f;                            // texel of the current cell = safe (render.frag:86: 1)
+    // one step of :94-128 -> the offset of the texel to load
+    auto advance = [&]() -> unsigned {
+        f0 = f0 + (r0 * tv) * len;                                                // :118
+        f1 = f1 + (r1 * tv) * len;
+        f2 = f2 + (r2 * tv) * len;
+        const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
+        f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;                              // :120
+        exy += __builtin_fmaf(fl1, xpf, fl0); e2 += fl2;                          // :119 (exact)
+        return __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy);
+    };
     int step = 0;                                                                // wave-uniform
-    constexpr bool kFract = VX_FRACT && SG >= 0;
-    if (kFract && maxs > 1) {                  // the first step, peeled: its len from march_len_sg
-        texel_t t;
-        VX_PAD_STEP(t, true)
-        len = march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2);
-        wait_vmem(t);
-        fetches += t >= 0 ? 1u : 0u;
+    const unsigned nl = active_lanes();
+    if (maxs > 1) {                            // the first step, peeled: its len from march_len_sg
+        const float t = ld_fmt1(rsrc, advance());                                  // :123-128
+        len = march_len_sg<SG>(S, f0, f1, f2);  // next step, under the load
+        cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
         tv = t;
-        witers += once_per_wave(1u);
+        cnt.march_witers += once_per_wave(1u);
+        cnt.march_slots += once_per_wave(nl);
         ++step;
     }
-    if (maxs > 1 && tv > 0 && step < maxs - 1) {
+    if (maxs > 1 && tv > 0.0f && step < maxs - 1) {
         do {
-            texel_t t;
-            VX_PAD_STEP(t, true)
-            len = (SG < 0 ? march_len(S, f0, f1, f2)
-                          : (kFract ? march_len_fract<(SG < 0 ? 0 : SG)>(S, f0, f1, f2)
-                                    : march_len_sg<(SG < 0 ? 0 : SG)>(S, f0, f1, f2)));   // next step, under the load
-            wait_vmem(t);
-            fetches += t >= 0 ? 1u : 0u;
+            const float t = ld_fmt1(rsrc, advance());
+            len = march_len_fract<SG>(S, f0, f1, f2);   // next step, under the load
+            cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
             tv = t;
-            witers += once_per_wave(1u);         // counted in the loop: step stays a scalar
-        } while (tv > 0 && ++step < maxs - 1);
+            cnt.march_witers += once_per_wave(1u);   // counted in the loop: step stays a scalar
+            cnt.march_slots += once_per_wave(nl);
+        } while (tv > 0.0f && ++step < maxs - 1);
     }
-    if (tv > 0) {                              // the MAX_STEPS-th step: only its fetch (stats) matters
-        texel_t t;                             // (a plain load: dropped unless counted)
-        VX_PAD_STEP(t, false)
-        fetches += t >= 0 ? 1u : 0u;
+    if (tv > 0.0f) {                           // the MAX_STEPS-th step: only its fetch (stats) matters
+        const float t = ld_fmt1(rsrc, advance());   // (dropped unless counted)
+        cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
     }
-#undef VX_PAD_STEP
-    return tv != 0;
+    return tv != 0.0f;
 }
 
 // march_pad with an LDS brick (VX_FLAG_SOFT_BRICK, the EXT 4 instantiation:
@@ -584,7 +413,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
 template <int SG>
 __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S, const int8_t *sun,
                                             const int8_t *brick, int ox, int oy, int oz, int c0, int c1, int c2,
-                                            float f0, float f1, float f2, unsigned &fetches, unsigned &witers) {
+                                            float f0, float f1, float f2, Counters &cnt) {
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = a.fc.max_steps;
     if (maxs <= 0) return maxs == 0;
@@ -598,6 +427,7 @@ __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S
     float len = march_len_sg<SG>(S, f0, f1, f2);
     int tv = 1;
     int step = 0;
+    const unsigned nl = active_lanes();
     bool first = true;
     do {
         const float safe = cvt_f32_ubyte0((uint32_t)tv);
@@ -616,12 +446,12 @@ __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S
             const unsigned off = __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(__builtin_fmaf(e1, xpf, e0));
             t = (int)ld_off(sunb, off);
         }
-        len = first ? march_len_sg<SG>(S, f0, f1, f2)
-                    : (VX_FRACT ? march_len_fract<SG>(S, f0, f1, f2) : march_len_sg<SG>(S, f0, f1, f2));
+        len = first ? march_len_sg<SG>(S, f0, f1, f2) : march_len_fract<SG>(S, f0, f1, f2);
         first = false;
-        fetches += t >= 0 ? 1u : 0u;
+        cnt.shadow_fetch += t >= 0 ? 1u : 0u;
         tv = t;
-        witers += once_per_wave(1u);
+        cnt.march_witers += once_per_wave(1u);
+        cnt.march_slots += once_per_wave(nl);
     } while (tv > 0 && ++step < maxs);
     // lit: left the grid (-1), or the MAX_STEPS-th step taken whatever it read
     // (render.frag:234: a block on the last step still ends with step == MAX_STEPS);
@@ -632,7 +462,7 @@ __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
 __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
-                              float f1, float f2, unsigned &fetches, unsigned &witers) {
+                              float f1, float f2, Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
     const float a0 = S.abs[0], a1 = S.abs[1], a2 = S.abs[2];
@@ -640,6 +470,7 @@ __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay 
     const int maxs = F.max_steps;
     float safe = 1.0f;
     int step = 0;
+    const unsigned nl = active_lanes();
     while (step < maxs && safe != 0.0f) {
         const float x0 = -f0 * s0, x1 = -f1 * s1, x2 = -f2 * s2;
         const float d0 = (x0 - floorf(x0)) + 1e-4f;
@@ -657,16 +488,14 @@ __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay 
         const float fl0 = floorf(f0), fl1 = floorf(f1), fl2 = floorf(f2);
         c0 += f2i(fl0); c1 += f2i(fl1); c2 += f2i(fl2);
         f0 = f0 - fl0; f1 = f1 - fl1; f2 = f2 - fl2;
-        if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) {
-            witers += once_per_wave((unsigned)step + 1u);
-            return true;
-        }
+        cnt.march_witers += once_per_wave(1u);
+        cnt.march_slots += once_per_wave(nl);
+        if (c0 >= a.X || c1 >= a.Y || c2 >= a.Z || c0 < 0 || c1 < 0 || c2 < 0) return true;
         const uint32_t t = sun[lin_index(a, c0, c1, c2)];
-        fetches++;
+        cnt.shadow_fetch++;
         safe = (float)t;
         step++;
     }
-    witers += once_per_wave((unsigned)step);
     return step == maxs;
 }
 
@@ -674,28 +503,22 @@ __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay 
 // S by value: the soft-shadow loop indexes sun_k[k] dynamically, and a
 // reference into the kernel argument there made the compiler copy the whole
 // KernelArgs (1.5 KB) to scratch.
-template <bool TAB>   // rstep points at an r*safe table of S (else the loop multiplies)
 __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
-                                          float f1, float f2, unsigned &fetches, unsigned &witers,
-                                          const float4 *rstep = nullptr) {
-    if (VX_MARCH_PAD && S.fast && a.sunp) {
+                                          float f1, float f2, Counters &cnt) {
+    if (S.fast && a.sunp) {
         const int8_t *ch = S.up ? a.sunp : a.sunp + a.sunp_texels;
-#if VX_MARCH_SG
         // wave-uniform switch on the frame's sun signs: one specialised loop each
         const int sg = (S.sign[0] > 0.0f ? 1 : 0) | (S.sign[1] > 0.0f ? 2 : 0) | (S.sign[2] > 0.0f ? 4 : 0);
         switch (sg) {
-#define VX_SG(K) case K: return march_pad<K, TAB>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rstep);
+#define VX_SG(K) case K: return march_pad<K>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
             VX_SG(0) VX_SG(1) VX_SG(2) VX_SG(3) VX_SG(4) VX_SG(5) VX_SG(6)
-            default: return march_pad<7, TAB>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rstep);
+            default: return march_pad<7>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
 #undef VX_SG
         }
-#else
-        return march_pad<-1, TAB>(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers, rstep);
-#endif
     }
     const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
-    return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers)
-                  : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, fetches, witers);
+    return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, cnt)
+                  : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
 }
 
 // ---------------- primary visibility ----------------
@@ -719,8 +542,6 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, i
 // d == 0 is a positive axis with iv = +inf: A - o >= 1 - o > 0 (0 <= o < 1 is
 // checked by vx_render), so tb = +inf exactly as the oracle's.  The box
 // [c, c + E*s] lies ahead of the ray: h and A bracket it on every axis.
-typedef float f2 __attribute__((ext_vector_type(2)));
-
 template <bool F32IDX>
 __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d2, Surf &g0, Surf &g1,
                        Counters &cnt) {
@@ -767,31 +588,6 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     const unsigned XpYp4 = 4u * a.XpYp;
     const unsigned kz = a.kz - XpYp4 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 2) - 0x4B000000u -
                         (XpYp4 << 22);
-#if VX_PRIM_TYPED
-    // the cell word through a typed load (8_8_8_8 USCALED, dst xyzw): colour and
-    // the three box extents arrive as exact fp32 integers, no byte converts in
-    // the loop; the colour logic runs on the float (the sentinel is 255.0)
-    // (F32IDX: the offset from a.prim carries the octant's copy; the integer
-    // path's per-lane copy base is no buffer base, so it converts the word)
-    const u32x4 prs = unorm_rsrc(a.prim, 0x52FACu);
-    auto fetch = [&](float x, float y, float z) -> f32x4 {
-        f32x4 v;
-        if (F32IDX) {
-            const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
-            const unsigned off = __umul24(__float_as_uint(z + 12582912.0f), XpYp4) + __float_as_uint(xy) + kz;
-            asm("buffer_load_format_xyzw %0, %1, %2, 0 offen\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(prs));
-        } else {
-            const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
-            const uint32_t w = ppad[(unsigned)idx];
-            v.x = cvt_f32_ubyte0(w); v.y = cvt_f32_ubyte1(w); v.z = cvt_f32_ubyte2(w); v.w = cvt_f32_ubyte3(w);
-        }
-        return v;
-    };
-    f32x4 t = fetch(h0, h1, h2);
-    cnt.prim_fetch++;
-    float prev = t.x;
-    float E0 = t.y, E1 = t.z, E2 = t.w;
-#else
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         if (F32IDX) {
             const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
@@ -803,27 +599,20 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     };
     uint32_t t = fetch(h0, h1, h2);
     cnt.prim_fetch++;
+    cnt.prim_witers += once_per_wave(1u);          // the entry fetch is a wave iteration too
     int prev = t & 0xff;
     float E0 = cvt_f32_ubyte1(t), E1 = cvt_f32_ubyte2(t), E2 = cvt_f32_ubyte3(t);
-#endif
     // gmark: the colour whose entry is "the first glass" -- glass until a glass
     // entry is recorded, then 256 (matches nothing).  The sentinel's colour
     // byte 0xFF is no vis colour (those are 0..21), so leaving the grid is an
     // entry that stops the walk.
-#if VX_PRIM_TYPED
-    float gmark = (float)kGlass, col;
-    int stop;
-#else
     int gmark = kGlass, stop, col;
-#endif
     float g0h = 0.0f, g1h = 0.0f, g2h = 0.0f, gt = 0.0f, te;
     float tb0, tb1, tb2;
     int gax = 0;
     const int cap = 4 * (a.X + a.Y + a.Z);
     int it = 0;
-    float pad_acc = 0.0f;
     do {
-        VX_PAD(VX_PAD_PRIM, pad_acc)
         // far face of the air box [c, c + E*s] ahead: A = h + s*E (exact)
         const float A0 = __builtin_fmaf(s0, E0, h0), A1 = __builtin_fmaf(s1, E1, h1), A2 = __builtin_fmaf(s2, E2, h2);
         tb0 = (A0 - o0) * iv0;
@@ -841,13 +630,8 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         h1 = e1 ? A1 + s1 : __builtin_amdgcn_fmed3f(q1, h1, A1);
         h2 = (!e0 && !e1) ? A2 + s2 : __builtin_amdgcn_fmed3f(q2, h2, A2);
         t = fetch(h0, h1, h2);
-#if VX_PRIM_TYPED
-        cnt.prim_fetch += t.x == 255.0f ? 0u : 1u;
-        col = t.x;
-#else
         cnt.prim_fetch += t >= kSentinel ? 0u : 1u;
         col = t & 0xff;
-#endif
         // a face of the mesh: entering a meshed cell (vis colour != 0) from a
         // cell of another colour; air is never meshed (sdf.cpp:229-233,284)
         const bool enter = col != prev && col != 0;
@@ -857,27 +641,16 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
             gax = e0 ? 0 : (e1 ? 1 : 2);
         }
         stop = (enter && col != kGlass) ? 1 : 0;       // later glass entries: single layer
-#if VX_STOP_VGPR
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
-#endif
         prev = col;
-#if VX_PRIM_TYPED
-        E0 = t.y; E1 = t.z; E2 = t.w;
-#else
         E0 = cvt_f32_ubyte1(t); E1 = cvt_f32_ubyte2(t); E2 = cvt_f32_ubyte3(t);
-#endif
         cnt.prim_witers += once_per_wave(1u);      // counted in the loop: it stays a scalar
     } while (stop == 0 && ++it < cap);
-    if (VX_PAD_PRIM) asm volatile("" ::"v"(pad_acc));
     // opaque after the loop: otherwise the compiler keeps the loop's compare
     // masks (stop, tb == te) alive past it, at 3 SALU merges per mask per step
     asm volatile("" : "+v"(col), "+v"(stop), "+v"(tb0), "+v"(tb1), "+v"(te));
     if (stop == 0) cnt.cap_hit++;
-#if VX_PRIM_TYPED
-    const bool hit = stop != 0 && col != 255.0f;
-#else
     const bool hit = stop != 0 && t < kSentinel;
-#endif
     const int hax = tb0 == te ? 0 : (tb1 == te ? 1 : 2);    // exit axis of the last step (ties x < y < z)
     // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
     int nrec = 0;
@@ -923,33 +696,31 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
     // AO coordinates are finite and far inside +-2^24 ((cell + fract) of a
     // fragment next to the grid): ivec3()'s NaN / saturation rules never
     // apply, so a plain convert is f2i here
-    const int i = VX_AO_CVT ? (int)fl : f2i(fl);
+    const int i = (int)fl;
     const int j = i + 1;
     i0 = min(max(i, 0), size - 1);
     i1 = min(max(j, 0), size - 1);
 }
 
 // sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G at LOD 0.
-__device__ __forceinline__ float sdf_lin(const KernelArgs &a, const float *unorm, int c0, int c1, int c2, float f0, float f1, float f2) {
+__device__ __forceinline__ float sdf_lin(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2) {
     const FrameConsts &F = a.fc;
     int x0, x1, y0, y1, z0, z1;
     float wx, wy, wz;
     lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
-#if VX_AO_DELTA
     // one byte offset and three deltas (0 or one row / plane / cell: the
     // clamped corners differ by at most one cell per axis)
     const unsigned b000 = lin_index(a, x0, y0, z0) << 1;
     const unsigned dx = (unsigned)(x1 - x0) << 1, dy = __umul24((unsigned)(y1 - y0), 2u * (unsigned)a.X),
                    dz = __umul24((unsigned)(z1 - z0), 2u * a.XY);
     const unsigned b010 = b000 + dy, b001 = b000 + dz, b011 = b010 + dz;
-#if VX_TYPED_UNORM
-    const u32x4 rs = unorm_rsrc(a.rg, kRsrcRG);
-    f32x2 u000 = ld_unorm2(rs, b000), u100 = ld_unorm2(rs, b000 + dx), u010 = ld_unorm2(rs, b010);
-    f32x2 u110 = ld_unorm2(rs, b010 + dx), u001 = ld_unorm2(rs, b001), u101 = ld_unorm2(rs, b001 + dx);
-    f32x2 u011 = ld_unorm2(rs, b011), u111 = ld_unorm2(rs, b011 + dx);
-    float ures[2];
+    const u32x4 rs = buf_rsrc(a.rg, kRsrcRG);
+    f32x2 u000 = ld_fmt2(rs, b000), u100 = ld_fmt2(rs, b000 + dx), u010 = ld_fmt2(rs, b010);
+    f32x2 u110 = ld_fmt2(rs, b010 + dx), u001 = ld_fmt2(rs, b001), u101 = ld_fmt2(rs, b001 + dx);
+    f32x2 u011 = ld_fmt2(rs, b011), u111 = ld_fmt2(rs, b011 + dx);
+    float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
         const float v00 = gmix(u000[ch], u100[ch], wx);
@@ -958,106 +729,41 @@ __device__ __forceinline__ float sdf_lin(const KernelArgs &a, const float *unorm
         const float v11 = gmix(u011[ch], u111[ch], wx);
         const float w0 = gmix(v00, v01, wy);
         const float w1 = gmix(v10, v11, wy);
-        ures[ch] = gmix(w0, w1, wz) * 255.0f;
-    }
-    return gmin(ures[0], ures[1]);
-#endif
-    auto ld = [&](unsigned off) -> uint32_t { return (uint32_t)ld_off(a.rg, off); };
-    const uint32_t t000 = ld(b000), t100 = ld(b000 + dx), t010 = ld(b010), t110 = ld(b010 + dx);
-    const uint32_t t001 = ld(b001), t101 = ld(b001 + dx), t011 = ld(b011), t111 = ld(b011 + dx);
-#else
-    auto ld = [&](int x, int y, int z) -> uint32_t { return (uint32_t)ld_off(a.rg, lin_index(a, x, y, z) << 1); };
-    const uint32_t t000 = ld(x0, y0, z0), t100 = ld(x1, y0, z0), t010 = ld(x0, y1, z0), t110 = ld(x1, y1, z0);
-    const uint32_t t001 = ld(x0, y0, z1), t101 = ld(x1, y0, z1), t011 = ld(x0, y1, z1), t111 = ld(x1, y1, z1);
-#endif
-    float res[2];
-#pragma unroll
-    for (int ch = 0; ch < 2; ch++) {
-        const int sh = 8 * ch;
-        const float v00 = gmix(unorm[(t000 >> sh) & 0xff], unorm[(t100 >> sh) & 0xff], wx);
-        const float v01 = gmix(unorm[(t010 >> sh) & 0xff], unorm[(t110 >> sh) & 0xff], wx);
-        const float v10 = gmix(unorm[(t001 >> sh) & 0xff], unorm[(t101 >> sh) & 0xff], wx);
-        const float v11 = gmix(unorm[(t011 >> sh) & 0xff], unorm[(t111 >> sh) & 0xff], wx);
-        const float w0 = gmix(v00, v01, wy);
-        const float w1 = gmix(v10, v11, wy);
         res[ch] = gmix(w0, w1, wz) * 255.0f;
     }
     return gmin(res[0], res[1]);
 }
 
 // REPEAT wrap of an integer-valued float onto [0, n), n a power of two:
-// floor(fl / n) with the IEEE quotient by n = 2^k, which is exactly fl * 2^-k
-// (fl is 0 or |fl| >= 1: no underflow), so the multiply by rn = 1/n (exact,
-// host-side) replaces a ~10-instruction correctly rounded division.
 // |fl| < 2^24 (every cloud lookup; a mountain lookup unless r1 ~ 0): fl - q*n
-// is exact and in [0, n), i.e. (int)fl mod n = (int)fl & (n - 1); the literal
-// form only for the lanes outside that range (NaN included).
-__device__ __forceinline__ int wrap_idx(float fl, int n, float rn) {
-    if (VX_WRAP_FAST) {
-        int r = (int)fl & (n - 1);
-        if (!(fabsf(fl) < 16777216.0f)) {
-            // 1/n from n (exact: a power of two), not from a kernel argument:
-            // a load sunk into this rare block would be tail-merged across the
-            // u/v calls into a pointer phi -- a KernelArgs copy to scratch
-            const float q = floorf(fl * (1.0f / (float)n));
-            r = f2i(fl - q * (float)n) & (n - 1);
-        }
-        return r;
+// is exact and in [0, n), i.e. (int)fl mod n = (int)fl & (n - 1).  The literal
+// form only for the lanes outside that range (NaN included): floor(fl / n)
+// with the IEEE quotient by n = 2^k, which is exactly fl * 2^-k (fl is 0 or
+// |fl| >= 1: no underflow).
+__device__ __forceinline__ int wrap_idx(float fl, int n) {
+    int r = (int)fl & (n - 1);
+    if (!(fabsf(fl) < 16777216.0f)) {
+        // 1/n from n (exact: a power of two), not from a kernel argument: a
+        // load sunk into this rare block would be tail-merged across the u/v
+        // calls into a pointer phi -- a KernelArgs copy to scratch
+        const float q = floorf(fl * (1.0f / (float)n));
+        r = f2i(fl - q * (float)n) & (n - 1);
     }
-    const float q = floorf(fl * rn);
-    return f2i(fl - q * (float)n) & (n - 1);
+    return r;
 }
 
 // fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT, LOD 0.
-#if VX_TYPED_UNORM && VX_SKY_BATCH
-// fbm in two halves, so the sky's four independent fbm samples (render.frag:
-// 188-189, 196-197) issue all their typed loads first: fbm_issue starts the
-// four A-texel loads and keeps the bilinear weights, fbm_finish blends them --
-// the same arithmetic as fbm.
-struct FbmTap {
-    float t[4];
-    float wa, wb;
-};
-__device__ __forceinline__ void fbm_issue(const KernelArgs &a, float px, float py, FbmTap &q) {
-    const int W = a.noise_w, H = a.noise_h;
-    const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
-    const float fu = floorf(u), fv = floorf(v);
-    q.wa = u - fu; q.wb = v - fv;
-    const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
-    const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-    const u32x4 rs = unorm_rsrc(a.noise, kRsrcA);
-    auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
-    q.t[0] = ld_unorm1(rs, off(x0, y0)); q.t[1] = ld_unorm1(rs, off(x1, y0));
-    q.t[2] = ld_unorm1(rs, off(x0, y1)); q.t[3] = ld_unorm1(rs, off(x1, y1));
-}
-__device__ __forceinline__ float fbm_finish(const FbmTap &q) {
-    const float r0 = gmix(q.t[0], q.t[1], q.wa), r1 = gmix(q.t[2], q.t[3], q.wa);
-    return 1.0f - 2.0f * gmix(r0, r1, q.wb);
-}
-#endif
-__device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, float px, float py) {
+__device__ __forceinline__ float fbm(const KernelArgs &a, float px, float py) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float wa = u - fu, wb = v - fv;
-    const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
+    const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-#if VX_TYPED_UNORM
-    const u32x4 rs = unorm_rsrc(a.noise, kRsrcA);
+    const u32x4 rs = buf_rsrc(a.noise, kRsrcA);
     auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
-    float t00 = ld_unorm1(rs, off(x0, y0)), t10 = ld_unorm1(rs, off(x1, y0));
-    float t01 = ld_unorm1(rs, off(x0, y1)), t11 = ld_unorm1(rs, off(x1, y1));
-#else
-    // A byte of texel (x, y): byte 4*(y*W + x) + 3, W = 2^noise_lw
-    auto ld = [&](int x, int y) -> uint32_t {
-        return (uint32_t)ld_off(reinterpret_cast<const uint8_t *>(a.noise),
-                                ((((unsigned)y << a.noise_lw) | (unsigned)x) << 2) + 3u);
-    };
-    const float t00 = unorm[ld(x0, y0)];
-    const float t10 = unorm[ld(x1, y0)];
-    const float t01 = unorm[ld(x0, y1)];
-    const float t11 = unorm[ld(x1, y1)];
-#endif
+    const float t00 = ld_fmt1(rs, off(x0, y0)), t10 = ld_fmt1(rs, off(x1, y0));
+    const float t01 = ld_fmt1(rs, off(x0, y1)), t11 = ld_fmt1(rs, off(x1, y1));
     const float r0 = gmix(t00, t10, wa), r1 = gmix(t01, t11, wa);
     return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
@@ -1070,16 +776,6 @@ __device__ __forceinline__ float fbm(const KernelArgs &a, const float *unorm, fl
 __device__ __forceinline__ float div_shared(float a, float b, float y) {
     return __builtin_copysignf(div_const(a, b, y), a);
 }
-
-#ifndef VX_NORM_MK
-#define VX_NORM_MK 1
-#endif
-#ifndef VX_UNORM_MK
-#define VX_UNORM_MK 1
-#endif
-#ifndef VX_ROUGH_RCP
-#define VX_ROUGH_RCP 1
-#endif
 
 // RN(1/l) for l with |l| in [2^-40, 2^41): v_rcp + one Newton step equals the
 // IEEE reciprocal on every such input (tools/micro/rcp_check.hip, exhaustive
@@ -1098,16 +794,12 @@ __device__ __forceinline__ void normalize3_ranged(float v0, float v1, float v2, 
 }
 __device__ __forceinline__ void normalize3(float v0, float v1, float v2, float &o0, float &o1, float &o2) {
     const float l = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
-    if (VX_NORM_MK) {               // one IEEE reciprocal, three exact corrections
-        const float y = 1.0f / l;
-        o0 = div_shared(v0, l, y); o1 = div_shared(v1, l, y); o2 = div_shared(v2, l, y);
-    } else {
-        o0 = v0 / l; o1 = v1 / l; o2 = v2 / l;
-    }
+    const float y = 1.0f / l;       // one IEEE reciprocal, three exact corrections
+    o0 = div_shared(v0, l, y); o1 = div_shared(v1, l, y); o2 = div_shared(v2, l, y);
 }
 
 // ---------------- render.frag main(), sky branch (render.frag:148-205) ----------------
-__device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unorm, float d0, float d1, float d2, float o[4],
+__device__ __forceinline__ void shade_sky(const KernelArgs &a, float d0, float d1, float d2, float o[4],
                           Counters &cnt) {
     const FrameConsts &F = a.fc;
     float r0, r1, r2;
@@ -1135,44 +827,23 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unor
     const float ct = F.cloudTime;
     const float den = sqrtf(fabsf(r2) + 0.03f);
     float sx, sy;                                                                 // :184
-    if (VX_NORM_MK) {
+    {
         const float y = 1.0f / den;
         sx = div_shared(r0, den, y); sy = div_shared(r1, den, y);
-    } else {
-        sx = r0 / den; sy = r1 / den;
     }
     sx = sx * 0.1f; sy = sy * 0.1f;
     const float sl = sqrtf(sqrtf(sx * sx + sy * sy));
     sx = sx * sl; sy = sy * sl;
-#if VX_TYPED_UNORM && VX_SKY_BATCH
-    // the four samples that do not depend on another fbm: their 16 loads first
-    const float mountainPos = r0 / r1;                                            // :195
-    FbmTap q0, q1, q3, q4;
-    fbm_issue(a, 2.0f * sx + ct, 2.0f * sy + ct, q0);
-    fbm_issue(a, 2.0f * sx - ct, 2.0f * sy - ct, q1);
-    fbm_issue(a, 0.3f * mountainPos, 0.3f * mountainPos, q3);
-    fbm_issue(a, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2), q4);
-    const float n0 = fbm_finish(q0);
-    const float n1 = fbm_finish(q1);
+    const float n0 = fbm(a, 2.0f * sx + ct, 2.0f * sy + ct);
+    const float n1 = fbm(a, 2.0f * sx - ct, 2.0f * sy - ct);
     sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
     sx = sx + F.skyOff[0];
     sy = sy + F.skyOff[1];
-    const float cloudFactor = vexp2(6.0f * (fbm(a, unorm, sx + 2.0f * ct, sy + -9.0f * ct) - 1.0f));
-    const float scf = sqrtf(cloudFactor);
-    float mountainHeight = 1.0f - fbm_finish(q3);
-    const float mountainFactor = 2.0f - fbm_finish(q4);
-#else
-    const float n0 = fbm(a, unorm, 2.0f * sx + ct, 2.0f * sy + ct);
-    const float n1 = fbm(a, unorm, 2.0f * sx - ct, 2.0f * sy - ct);
-    sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
-    sx = sx + F.skyOff[0];
-    sy = sy + F.skyOff[1];
-    const float cloudFactor = vexp2(6.0f * (fbm(a, unorm, sx + 2.0f * ct, sy + -9.0f * ct) - 1.0f));
+    const float cloudFactor = vexp2(6.0f * (fbm(a, sx + 2.0f * ct, sy + -9.0f * ct) - 1.0f));
     const float scf = sqrtf(cloudFactor);
     const float mountainPos = r0 / r1;                                            // :195
-    float mountainHeight = 1.0f - fbm(a, unorm, 0.3f * mountainPos, 0.3f * mountainPos);
-    const float mountainFactor = 2.0f - fbm(a, unorm, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2));
-#endif
+    float mountainHeight = 1.0f - fbm(a, 0.3f * mountainPos, 0.3f * mountainPos);
+    const float mountainFactor = 2.0f - fbm(a, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2));
     mountainHeight = mountainHeight / (vexp(0.3f * mountainPos * mountainPos) * 6.0f);
     if (mountainHeight > r2 && r1 > 0.0f && r2 > 0.0f) {
         const float mt[3] = {0.7f, 0.8f, 0.7f};
@@ -1188,38 +859,24 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, const float *unor
 
 // ---------------- extensions (DESIGN.md §3 "Extensions") ----------------
 // white(p) = 1 - 2*texture(u_noise, p).rgb (render.frag:16-21), bilinear REPEAT LOD 0.
-__device__ __forceinline__ void white(const KernelArgs &a, const float *unorm, float px, float py, float &w0, float &w1, float &w2) {
+__device__ __forceinline__ void white(const KernelArgs &a, float px, float py, float &w0, float &w1, float &w2) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float wa = u - fu, wb = v - fv;
-    const int x0 = wrap_idx(fu, W, a.noise_rw), y0 = wrap_idx(fv, H, a.noise_rh);
+    const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
     const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
     float w[3];
-#if VX_TYPED_UNORM
-    const u32x4 rs = unorm_rsrc(a.noise, kRsrcRGB);
+    const u32x4 rs = buf_rsrc(a.noise, kRsrcRGB);
     auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
-    f32x3 u00 = ld_unorm3(rs, off(x0, y0)), u10 = ld_unorm3(rs, off(x1, y0));
-    f32x3 u01 = ld_unorm3(rs, off(x0, y1)), u11 = ld_unorm3(rs, off(x1, y1));
+    f32x3 u00 = ld_fmt3(rs, off(x0, y0)), u10 = ld_fmt3(rs, off(x1, y0));
+    f32x3 u01 = ld_fmt3(rs, off(x0, y1)), u11 = ld_fmt3(rs, off(x1, y1));
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
         const float r0 = gmix(u00[ch], u10[ch], wa);
         const float r1 = gmix(u01[ch], u11[ch], wa);
         w[ch] = 1.0f - 2.0f * gmix(r0, r1, wb);
     }
-#else
-    auto ld = [&](int x, int y) -> uint32_t {
-        return ld_off(a.noise, (((unsigned)y << a.noise_lw) | (unsigned)x) << 2);
-    };
-    const uint32_t t00 = ld(x0, y0), t10 = ld(x1, y0), t01 = ld(x0, y1), t11 = ld(x1, y1);
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) {
-        const int sh = 8 * ch;
-        const float r0 = gmix(unorm[(t00 >> sh) & 0xff], unorm[(t10 >> sh) & 0xff], wa);
-        const float r1 = gmix(unorm[(t01 >> sh) & 0xff], unorm[(t11 >> sh) & 0xff], wa);
-        w[ch] = 1.0f - 2.0f * gmix(r0, r1, wb);
-    }
-#endif
     w0 = w[0]; w1 = w[1]; w2 = w[2];
 }
 
@@ -1234,7 +891,7 @@ constexpr float kRoughAmp = 0.1f;
 // normal, exactly as shade_block computes it: the soft-shadow pass of k_render
 // asks it first, to know which fragments march.
 template <int EXT>
-__device__ __forceinline__ float block_shade_factor(const KernelArgs &a, const float *unorm, const Surf &g) {
+__device__ __forceinline__ float block_shade_factor(const KernelArgs &a, const Surf &g) {
     const FrameConsts &F = a.fc;
     const int ni = g.nidx;
     if (!(EXT && (F.flags & VX_FLAG_ROUGH))) return F.shadeFactor[ni];
@@ -1245,18 +902,15 @@ __device__ __forceinline__ float block_shade_factor(const KernelArgs &a, const f
     const float u = ax == 0 ? (float)g.c1 + g.f1 : (float)g.c0 + g.f0;
     const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;
     float w0, w1, w2, m0, m1, m2;
-    white(a, unorm, u * kRoughScale, v * kRoughScale, w0, w1, w2);
-    if (VX_ROUGH_RCP)
-        normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
-    else
-        normalize3(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+    white(a, u * kRoughScale, v * kRoughScale, w0, w1, w2);
+    normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
     return F.sun[2] < 0.0f ? 0.0f : sqrtf(gmax(0.0f, (m0 * F.sun[0] + m1 * F.sun[1]) + m2 * F.sun[2]));
 }
 
 // lit_given >= 0 (EXT 2): the soft-shadow samples of this fragment were
 // marched by k_render's wave pass, lit_given of them lit.
 template <int EXT>
-__device__ __forceinline__ void shade_block(const KernelArgs &a, const float *unorm, const Surf &g, float o[4], Counters &cnt,
+__device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, float o[4], Counters &cnt,
                             bool has_ray = false, float q0 = 0.0f, float q1 = 0.0f, float q2 = 0.0f,
                             float *ray_out = nullptr, int lit_given = -1) {
     const FrameConsts &F = a.fc;
@@ -1282,19 +936,16 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const float *un
         const float u = ax == 0 ? (float)g.c1 + g.f1 : (float)g.c0 + g.f0;   // first in-face axis
         const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;   // second
         float w0, w1, w2;
-        white(a, unorm, u * kRoughScale, v * kRoughScale, w0, w1, w2);
+        white(a, u * kRoughScale, v * kRoughScale, w0, w1, w2);
         // |n + 0.1 w| lies in [0.89, 1.11] (unit axis n, |w_i| <= 1): rcp_ranged is exact
-        if (VX_ROUGH_RCP)
-            normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
-        else
-            normalize3(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
+        normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
     }
     float base0 = 1.0f, base1 = 1.0f, base2 = 1.0f;
     if (g.color < 22) { base0 = kPalette[g.color][0]; base1 = kPalette[g.color][1]; base2 = kPalette[g.color][2]; }
     float amb0 = 1.0f, amb1 = 1.0f, amb2 = 1.0f;
     if (!(F.flags & VX_FLAG_NO_AO)) {                                                  // :223-225
         cnt.ao++;
-        const float ambDist = sdf_lin(a, unorm, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
+        const float ambDist = sdf_lin(a, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
         const float ambFactor = gmin(1.0f - sqrtf(ambDist), 0.8f);
         amb0 = gmix(1.0f, F.shadeCol[0], ambFactor);
         amb1 = gmix(1.0f, F.shadeCol[1], ambFactor);
@@ -1306,8 +957,7 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const float *un
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
         if (EXT != 2) {                // the reference's hard shadow: one sun ray
             cnt.shadow_rays++;
-            const bool lit = march_sun<VX_RSTEP != 0>(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
-                                       cnt.march_witers, reinterpret_cast<const float4 *>(unorm + 256));
+            const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt);
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
         } else if (lit_given >= 0) {   // marched by the wave pass (k_render)
             shadeFactor = shadeFactor * ((float)lit_given / (float)F.n_sun);
@@ -1315,8 +965,7 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const float *un
             int lit = 0;
             for (int k = 0; k < F.n_sun; k++) {
                 cnt.shadow_rays++;
-                lit += march_sun<false>(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt.shadow_fetch,
-                                        cnt.march_witers) ? 1 : 0;
+                lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt) ? 1 : 0;
             }
             shadeFactor = shadeFactor * ((float)lit / (float)F.n_sun);
         }
@@ -1418,7 +1067,7 @@ __device__ __forceinline__ int walk_reflect(const KernelArgs &a, int B0, int B1,
 // (rd = the camera rayDir at the fragment; R = rd with the face-axis
 // component negated = reflect(rd, n) exactly), oracle reflect_color().
 template <int EXT>
-__device__ __forceinline__ void reflect_color(const KernelArgs &a, const float *unorm, const Surf &gl, const float rd[3], float out[3],
+__device__ __forceinline__ void reflect_color(const KernelArgs &a, const Surf &gl, const float rd[3], float out[3],
                               Counters &cnt) {
     const int ax = gl.nidx >> 1;
     const float R0 = ax == 0 ? -rd[0] : rd[0], R1 = ax == 1 ? -rd[1] : rd[1], R2 = ax == 2 ? -rd[2] : rd[2];
@@ -1436,9 +1085,9 @@ __device__ __forceinline__ void reflect_color(const KernelArgs &a, const float *
     Surf h;
     float rgba[4];
     if (walk_reflect(a, B0, B1, B2, o0, o1, o2, R0, R1, R2, s0, s1, s2, h, cnt))
-        shade_block<EXT>(a, unorm, h, rgba, cnt, true, R0, R1, R2);
+        shade_block<EXT>(a, h, rgba, cnt, true, R0, R1, R2);
     else
-        shade_sky(a, unorm, R0, R1, R2, rgba, cnt);
+        shade_sky(a, R0, R1, R2, rgba, cnt);
     out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
 }
 
@@ -1553,45 +1202,27 @@ __device__ __forceinline__ void shade_2d(const KernelArgs &a, float d0, float d1
 
 // Lane = pixel, wave = 8x8 tile, workgroup = 32x8 pixels.
 // EXT: 0 = v1 (the reference's shader), 1 = extensions (REFLECT, ROUGH) with
-// the hard shadow, 2 = extensions with soft shadows (n sun samples).  Each
+// the hard shadow, 2 = extensions with soft shadows (n sun samples), 3 = 2 with
+// the first surface's samples marched by the pooled wave pass
+// (VX_FLAG_SOFT_POOL), 4 = 3 with LDS brick staging (VX_FLAG_SOFT_BRICK).  Each
 // instantiation carries only its own code and registers; soft shadows in a
 // kernel of their own also keep the sun_k[0] / sun_k[k] addresses apart (a
 // pointer phi between them makes the compiler copy KernelArgs to scratch).
 // Occupancy: 8 waves/SIMD needs <= 64 VGPRs and <= 80 SGPRs (8 256-thread
-// blocks per CU, MI355X_MICROARCH.md "Residency"); the EXT instantiation is
-// held to that budget explicitly (left alone it takes 66 VGPRs + 100 SGPRs
-// and runs at 6 waves/SIMD).
-#ifndef VX_EXT_OCC
-#define VX_EXT_OCC 1
-#endif
-#if VX_EXT_OCC
+// blocks per CU, MI355X_MICROARCH.md "Residency"); every instantiation is held
+// to that budget explicitly (left alone the EXT ones take 66 VGPRs + 100 SGPRs
+// and run at 6 waves/SIMD).
 #define VX_OCC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_sgpr(80)))
-#else
-#define VX_OCC_ATTR
-#endif
 // Workgroup = 256 threads = four 8x8-pixel waves side by side: a 32x8 pixel
-// block (VX_BX = 32; 16 gives the round-1 16x16 block).  A 32-pixel block row
-// is 128 B of RGBA8: the framebuffer store goes through LDS so every wave
-// writes two whole 128-B rows (full cache lines) instead of eight 32-B
-// pieces of its own 8x8 tile (VX_STAGE).
-#ifndef VX_BX
-#define VX_BX 32
-#endif
-#ifndef VX_SOFT_TAB
-#define VX_SOFT_TAB 0
-#endif
-#ifndef VX_POOL
-#define VX_POOL 0
-#endif
-#ifndef VX_STAGE
-#define VX_STAGE 1
-#endif
-constexpr int kBX = VX_BX;                 // block width in pixels (16 or 32)
+// block.  A 32-pixel block row is 128 B of RGBA8: the framebuffer store goes
+// through LDS so every wave writes two whole 128-B rows (full cache lines)
+// instead of eight 32-B pieces of its own 8x8 tile.
+constexpr int kBX = 32;                    // block width in pixels
 constexpr int kBY = kWG / kBX;             // block height
-constexpr int kBXS = kBX == 32 ? 5 : 4;    // log2(kBX)
-constexpr int kBYS = kBY == 8 ? 3 : 4;     // log2(kBY)
+constexpr int kBXS = 5;                    // log2(kBX)
+constexpr int kBYS = 3;                    // log2(kBY)
 constexpr int kWX = kBX / 8;               // waves per block row
-static_assert(kBX == 16 || kBX == 32, "VX_BX must be 16 or 32");
+static_assert(kBX == 1 << kBXS && kBY == 1 << kBYS, "block shape");
 
 // F32IDX: the fp32 primary index (a.prim_f32) -- a kernel of its own: two
 // inlined primary() copies in one kernel make the compiler copy KernelArgs
@@ -1599,20 +1230,12 @@ static_assert(kBX == 16 || kBX == 32, "VX_BX must be 16 or 32");
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
 __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
-    // EXT 3 (VX_FLAG_SOFT_POOL): the soft-shadow instantiation (EXT 2) with the
-    // first surface's samples marched by the pooled wave pass
-    constexpr int XE = EXT >= 3 ? 2 : EXT;
-    constexpr bool kPoolOn = EXT >= 3 || (EXT == 2 && VX_POOL);
+    constexpr int XE = EXT >= 3 ? 2 : EXT;     // the shading instantiation (EXT 3/4 shade as 2)
+    constexpr bool kPool = EXT >= 3;           // VX_FLAG_SOFT_POOL: the pooled wave pass
     constexpr bool kBrick = EXT == 4;          // VX_FLAG_SOFT_BRICK: + LDS brick staging
-    // LDS: [0, 256) unorm8 -> float table, b/255 as IEEE quotients (render.frag:38
-    // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
-    // decode); then 128 float4 (r*k) of the frame's sun for march_pad (k = safe)
-    __shared__ float4 s_lds[64 + (VX_RSTEP ? 128 : 0)];
     __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
-    __shared__ float4 s_rk[XE == 2 && VX_SOFT_TAB ? 4 * 128 : 1];   // EXT 2: per wave, r*k of the current sample
-    // EXT 2, VX_POOL: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
+    // pooled pass: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
     // the compacted marching fragments' start (fract, cell) and lit counts
-    constexpr int kPool = kPoolOn ? 1 : 0;
     __shared__ float4 s_sunk[kPool ? 3 * VX_MAX_SHADOW_SAMPLES : 1];
     __shared__ float4 s_pf[kPool ? kWG : 1];
     __shared__ int4 s_pc[kPool ? kWG : 1];
@@ -1627,17 +1250,8 @@ void k_render(KernelArgs a) {
                 s_sunk[3 * k + 2] = make_float4(Sk.rcp[0], Sk.rcp[1], Sk.rcp[2], 0.0f);
             }
         }
+        __syncthreads();
     }
-    float *s_unorm = reinterpret_cast<float *>(s_lds);
-#pragma unroll
-    for (int i = threadIdx.x; i < 256; i += kWG)        // = (float)i / 255.0f, the IEEE quotient (§5)
-        s_unorm[i] = VX_UNORM_MK ? div_const((float)i, 255.0f, 1.0f / 255.0f) : (float)i / 255.0f;
-    if (VX_RSTEP && threadIdx.x < 128) {
-        const float k = (float)threadIdx.x;
-        const SunRay &S0 = a.fc.sun_k[0];
-        s_lds[64 + threadIdx.x] = make_float4(S0.r[0] * k, S0.r[1] * k, S0.r[2] * k, 0.0f);
-    }
-    __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lx = ((wave % kWX) << 3) | (lane & 7);
     const int ly = ((wave / kWX) << 3) | (lane >> 3);
@@ -1660,56 +1274,33 @@ void k_render(KernelArgs a) {
         oy = blockIdx.y << kBYS;
     }
     const int px = ox + lx, py = oy + ly;
+    const bool inframe = px < a.w && py < a.h;
     const FrameConsts &F = a.fc;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {};
     unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
-    if (px < a.w && py < a.h) {
+    // The pooled pass deals work over all 64 lanes of a wave, so there every
+    // lane runs: a lane off the frame (a partial edge wave) takes the nearest
+    // in-frame pixel's ray, marches for the others, and neither counts its own
+    // primary work nor shades nor stores.
+    if (kPool || inframe) {
         float d0, d1, d2;
-        view_ray(F, px, py, d0, d1, d2);
+        view_ray(F, kPool ? min(px, a.w - 1) : px, kPool ? min(py, a.h - 1) : py, d0, d1, d2);
         // the field copy of this ray's octant (zero components count positive)
         const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
         Surf g[2];
         const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt);
-        // EXT 2 (soft shadows): the samples of the first surface marched here,
-        // one sample at a time for the whole wave, each with an LDS table of its
-        // r*safe products built by all 64 lanes (the march_pad TAB form of the
-        // hard shadow).  Later surfaces (behind glass, in a reflection) march
-        // in shade_block.
         int lit0 = -1;
-        if (XE == 2 && VX_SOFT_TAB) {
-            const bool need = n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
-                              block_shade_factor<XE>(a, s_unorm, g[0]) > 0.0f;
-            if (__ballot(need)) {
-                lit0 = 0;
-                float4 *tab = s_rk + (threadIdx.x & ~63) * 2;
-                for (int k = 0; k < F.n_sun; k++) {
-                    const SunRay S = F.sun_k[k];
-                    const float k0 = (float)lane, k1 = (float)(lane + 64);
-                    tab[lane] = make_float4(S.r[0] * k0, S.r[1] * k0, S.r[2] * k0, 0.0f);
-                    tab[lane + 64] = make_float4(S.r[0] * k1, S.r[1] * k1, S.r[2] * k1, 0.0f);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    if (need) {
-                        cnt.shadow_rays++;
-                        lit0 += march_sun<true>(a, S, g[0].c0, g[0].c1, g[0].c2, g[0].f0, g[0].f1, g[0].f2,
-                                                cnt.shadow_fetch, cnt.march_witers, tab) ? 1 : 0;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                }
-                if (!need) lit0 = -1;
-            }
-        }
-        if (kPoolOn && !VX_SOFT_TAB && F.soft_sg >= 0 && a.sunp) {
-            // Pooled soft shadows (VX_POOL): the fragments of the wave that march
-            // are compacted by a ballot, and each pass deals 64 / G of them with
+        if (kPool && !inframe) cnt = Counters{};
+        if (kPool && F.soft_sg >= 0 && a.sunp) {
+            // Pooled soft shadows: the fragments of the wave that march are
+            // compacted by a ballot, and each pass deals 64 / G of them with
             // G = 2^soft_lg lanes per fragment, lane k of a group marching sample
             // k.  A wave load then touches the few cache lines around 64 / G
             // surface points instead of one line per pixel, and lanes whose own
             // pixel does not march (sky, faces turned from the sun) march for
             // the others.  Same exact march_pad, lit counted per fragment in LDS.
-            const bool need = n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
-                              block_shade_factor<XE>(a, s_unorm, g[0]) > 0.0f;
+            const bool need = inframe && n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
+                              block_shade_factor<XE>(a, g[0]) > 0.0f;
             const unsigned long long mask = __ballot(need);
             if (mask) {
                 const int wb = threadIdx.x & ~63;                // this wave's 64 slots
@@ -1733,13 +1324,12 @@ void k_render(KernelArgs a) {
                 const int8_t *ch = F.sun_k[0].up ? a.sunp : a.sunp + a.sunp_texels;
                 // EXT 4 is launched only when the bricks fit (launch_render): <= 4 fragments per
                 // pass, 4-byte aligned rows, a border of >= 9 cells around the grid
-                constexpr bool brick_on = kBrick;
                 const int sgv = F.soft_sg;
                 const int bx = (sgv & 1) ? 0 : 4, by = (sgv & 2) ? 1 : 6, bz = (sgv & 4) ? 1 : 6;
                 const int fpp = 64 >> lg;
                 for (int base = 0; base < nf; base += fpp) {          // wave-uniform passes
                     const int fs = base + (lane >> lg);
-                    if (kBrick && brick_on) {
+                    if (kBrick) {
                         // stage the pass's bricks: 4 x 64 rows x 2 dwords, 8 dword loads per lane
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
@@ -1763,26 +1353,27 @@ void k_render(KernelArgs a) {
                         const int4 pc = s_pc[wb + fs];
                         cnt.shadow_rays++;
                         bool lit;
-                        if (kBrick && brick_on) {
+                        if constexpr (kBrick) {
                             const int8_t *br = reinterpret_cast<const int8_t *>(s_brick + (wb >> 6) * 512) +
                                                512 * (lane >> lg);
                             const int ox = (pc.x + a.SB - bx) & ~3, oy = pc.y + a.SB - by, oz = pc.z + a.SB - bz;
                             switch (sgv) {
 #define VX_SGB(K) case K: lit = march_brick<K>(a, S, ch, br, ox, oy, oz, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
-                                               cnt.shadow_fetch, cnt.march_witers); break;
+                                               cnt); break;
                                 VX_SGB(0) VX_SGB(1) VX_SGB(2) VX_SGB(3) VX_SGB(4) VX_SGB(5) VX_SGB(6)
                                 default: lit = march_brick<7>(a, S, ch, br, ox, oy, oz, pc.x, pc.y, pc.z, pf.x, pf.y,
-                                                              pf.z, cnt.shadow_fetch, cnt.march_witers);
+                                                              pf.z, cnt);
 #undef VX_SGB
                             }
-                        } else if constexpr (!kBrick)
-                        switch (F.soft_sg) {
-#define VX_SGP(K) case K: lit = march_pad<K, false>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
-                                                    cnt.shadow_fetch, cnt.march_witers, nullptr); break;
-                            VX_SGP(0) VX_SGP(1) VX_SGP(2) VX_SGP(3) VX_SGP(4) VX_SGP(5) VX_SGP(6)
-                            default: lit = march_pad<7, false>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
-                                                               cnt.shadow_fetch, cnt.march_witers, nullptr);
+                        } else {
+                            switch (sgv) {
+#define VX_SGP(K) case K: lit = march_pad<K>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
+                                             cnt); break;
+                                VX_SGP(0) VX_SGP(1) VX_SGP(2) VX_SGP(3) VX_SGP(4) VX_SGP(5) VX_SGP(6)
+                                default: lit = march_pad<7>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
+                                                            cnt);
 #undef VX_SGP
+                            }
                         }
                         if (lit) atomicAdd(&s_plit[wb + fs], 1);
                     }
@@ -1792,50 +1383,51 @@ void k_render(KernelArgs a) {
                 if (need) lit0 = s_plit[wb + slot];
             }
         }
-        float rgba[4];
-        if (F.flags & VX_FLAG_PRIMARY_ONLY) {
-            primary_only_colour(n, g[0], rgba);
-            n_sky = n == 0;
-            n_glass = n != 0 && g[0].id == 2;
-            n_block = n != 0 && g[0].id != 2;
-        } else if (n == 0) {
-            n_sky = 1;
-            shade_sky(a, s_unorm, d0, d1, d2, rgba, cnt);
-        } else {
-            float rd[3];
-            shade_block<XE>(a, s_unorm, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
-            if (g[0].id == 2) {
-                n_glass = 1;
-                if (XE && (F.flags & VX_FLAG_REFLECT)) {
-                    // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
-                    float refl[3];
-                    reflect_color<XE>(a, s_unorm, g[0], rd, refl, cnt);
-                    const int ax = g[0].nidx >> 1;
-                    const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
-                    const float x = 1.0f - cs, x2 = x * x;
-                    const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
-#pragma unroll
-                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
-                }
-                float dst[4];
-                if (n == 2) shade_block<XE>(a, s_unorm, g[1], dst, cnt);
-                else shade_sky(a, s_unorm, d0, d1, d2, dst, cnt);
-                const float al = rgba[3];
-#pragma unroll
-                for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+        if (!kPool || inframe) {
+            float rgba[4];
+            if (F.flags & VX_FLAG_PRIMARY_ONLY) {
+                primary_only_colour(n, g[0], rgba);
+                n_sky = n == 0;
+                n_glass = n != 0 && g[0].id == 2;
+                n_block = n != 0 && g[0].id != 2;
+            } else if (n == 0) {
+                n_sky = 1;
+                shade_sky(a, d0, d1, d2, rgba, cnt);
             } else {
-                n_block = 1;
+                float rd[3];
+                shade_block<XE>(a, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
+                if (g[0].id == 2) {
+                    n_glass = 1;
+                    if (XE && (F.flags & VX_FLAG_REFLECT)) {
+                        // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
+                        float refl[3];
+                        reflect_color<XE>(a, g[0], rd, refl, cnt);
+                        const int ax = g[0].nidx >> 1;
+                        const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
+                        const float x = 1.0f - cs, x2 = x * x;
+                        const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
+#pragma unroll
+                        for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
+                    }
+                    float dst[4];
+                    if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
+                    else shade_sky(a, d0, d1, d2, dst, cnt);
+                    const float al = rgba[3];
+#pragma unroll
+                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+                } else {
+                    n_block = 1;
+                }
             }
+            rgba[3] = 1.0f;
+            if (FMT == VX_PIXEL_RGBA8)
+                s_px[ly][lx] = pack_rgba8(rgba);
+            else
+                store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
+            n_px = 1;
         }
-        rgba[3] = 1.0f;
-        if (FMT == VX_PIXEL_RGBA8 && VX_STAGE) {
-            s_px[ly][lx] = pack_rgba8(rgba);
-        } else {
-            store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
-        }
-        n_px = 1;
     }
-    if (FMT == VX_PIXEL_RGBA8 && VX_STAGE) {
+    if (FMT == VX_PIXEL_RGBA8) {
         // block -> framebuffer in whole rows: thread t stores pixel (t % kBX, t / kBX)
         // of the block, so a wave writes two contiguous kBX*4-byte rows
         __syncthreads();
@@ -1861,6 +1453,7 @@ void k_render(KernelArgs a) {
         v[ST_ROUGH] = wave_sum(cnt.rough);
         v[ST_PRIM_WITERS] = wave_sum(cnt.prim_witers);
         v[ST_MARCH_WITERS] = wave_sum(cnt.march_witers);
+        v[ST_MARCH_SLOTS] = wave_sum(cnt.march_slots);
         if (lane == 0) {
             // spread the adds over 64 slot rows to avoid one hot line per counter
             unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
@@ -1895,19 +1488,19 @@ __global__ __launch_bounds__(kWG) void k_render_2d(KernelArgs a) {
         oy = blockIdx.y << kBYS;
     }
     const int px = ox + lx, py = oy + ly;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {};
     unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
     if (px < a.w && py < a.h) {
         float d0, d1, d2, rgba[4];
         view_ray(a.fc, px, py, d0, d1, d2);
         shade_2d(a, d0, d1, d2, rgba, cnt, n_sky, n_block, n_glass);
-        if (FMT == VX_PIXEL_RGBA8 && VX_STAGE)
+        if (FMT == VX_PIXEL_RGBA8)
             s_px[ly][lx] = pack_rgba8(rgba);
         else
             store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
         n_px = 1;
     }
-    if (FMT == VX_PIXEL_RGBA8 && VX_STAGE) {
+    if (FMT == VX_PIXEL_RGBA8) {
         __syncthreads();
         const int sx = threadIdx.x & (kBX - 1), sy = threadIdx.x >> kBXS;
         if (ox + sx < a.w && oy + sy < a.h)
@@ -2138,17 +1731,8 @@ __global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)X * Y * Z) return;
     const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
-#if VX_SUN_BRICK
-    // 8x4x4 bricks, one 128-B line each (march_pad); padded extents rounded to whole bricks
-    const size_t Xp = ((size_t)X + 2 * SB + 7) & ~(size_t)7, Yp = ((size_t)Y + 2 * SB + 3) & ~(size_t)3;
-    const size_t Zp = ((size_t)Z + 2 * SB + 3) & ~(size_t)3;
-    const size_t px = (size_t)(x + SB), py = (size_t)(y + SB), pz = (size_t)(z + SB);
-    const size_t j = ((((pz >> 2) * (Yp >> 2) + (py >> 2)) * (Xp >> 3) + (px >> 3)) << 7) | ((pz & 3) << 5) |
-                     ((py & 3) << 3) | (px & 7);
-#else
     const size_t Xp = (size_t)X + 2 * SB, Yp = (size_t)Y + 2 * SB, Zp = (size_t)Z + 2 * SB;
     const size_t j = (size_t)(x + SB) + Xp * ((size_t)(y + SB) + Yp * (size_t)(z + SB));
-#endif
     const uint32_t t = src[i];
     sunp[j] = (int8_t)(t & 0xffu);
     sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);

@@ -55,6 +55,31 @@ int vx_mgpu_bands(int h, int band_rows, int nranks, int rank, int *ids, int cap)
     return n;
 }
 
+int vx_mgpu_transfers(int w, int h, int band_rows, int pixel_format, int nranks, int rank, vx_mgpu_xfer *out,
+                      int cap) {
+    if (w <= 0 || h <= 0 || band_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || cap < 0 ||
+        (pixel_format != VX_PIXEL_RGBA8 && pixel_format != VX_PIXEL_RGBA32F))
+        return set_error(VX_EINVAL, "vx_mgpu_transfers: bad arguments");
+    const uint64_t row_bytes = (uint64_t)w * (pixel_format == VX_PIXEL_RGBA32F ? 16u : 4u);
+    const int nb = (h + band_rows - 1) / band_rows;
+    int n = 0;
+    for (int b = 0; b < nb; b++) {
+        const int owner = b % nranks;
+        if (owner == 0 || (rank != 0 && owner != rank)) continue;
+        if (out && n < cap) {
+            vx_mgpu_xfer &x = out[n];
+            x.band = b;
+            x.src = owner;
+            x.dst = 0;
+            x.rows = (b + 1) * band_rows <= h ? band_rows : h - b * band_rows;
+            x.offset = (uint64_t)b * band_rows * row_bytes;
+            x.bytes = (uint64_t)x.rows * row_bytes;
+        }
+        n++;
+    }
+    return n;
+}
+
 int vx_mgpu_unique_id(void *uid) {
     if (!uid) return set_error(VX_EINVAL, "vx_mgpu_unique_id: null argument");
     ncclUniqueId id;
@@ -106,6 +131,9 @@ int vx_mgpu_render(vx_mgpu *m, const vx_frame_params *p, int w, int h, int band_
         m->band_rows = band_rows;
     }
     if (hipSetDevice(m->device) != hipSuccess) return set_error(VX_EDEVICE, "vx_mgpu_render: hipSetDevice failed");
+    // one stream for the render and the gather: NULL means the scene's own
+    // stream (non-blocking), which the legacy null stream would not wait for
+    if (!stream) stream = scene_stream(m->scene);
     if (!m->mine.empty()) {
         const int rc = vx_render_bands(m->scene, p, w, h, band_rows, m->mine.data(), (int)m->mine.size(),
                                        pixel_format, frame_device, 1, stream, stats);
@@ -125,31 +153,20 @@ int vx_mgpu_gather(vx_mgpu *m, int w, int h, int band_rows, int pixel_format, vo
         return set_error(VX_EINVAL, "vx_mgpu_gather: unknown pixel format");
     if (m->nranks == 1) return VX_OK;
     if (hipSetDevice(m->device) != hipSuccess) return set_error(VX_EDEVICE, "vx_mgpu_gather: hipSetDevice failed");
-    hipStream_t st = (hipStream_t)stream;
+    hipStream_t st = (hipStream_t)(stream ? stream : scene_stream(m->scene));
     // the gather: every band not rank 0's goes from its owner's frame rows to rank 0's
-    const size_t px = pixel_format == VX_PIXEL_RGBA32F ? 16 : 4;
-    const size_t row_bytes = (size_t)w * px;
+    const int n = vx_mgpu_transfers(w, h, band_rows, pixel_format, m->nranks, m->rank, nullptr, 0);
+    std::vector<vx_mgpu_xfer> xs(n > 0 ? n : 0);
+    if (n > 0) vx_mgpu_transfers(w, h, band_rows, pixel_format, m->nranks, m->rank, xs.data(), n);
     char *frame = static_cast<char *>(frame_device);
-    const int nb = (h + band_rows - 1) / band_rows;
     VX_NCCL(ncclGroupStart());
-    for (int b = 0; b < nb; b++) {
-        const int owner = b % m->nranks;
-        if (owner == 0) continue;
-        const int rows = (b + 1) * band_rows <= h ? band_rows : h - b * band_rows;
-        char *ptr = frame + (size_t)b * band_rows * row_bytes;
-        const size_t bytes = (size_t)rows * row_bytes;
-        if (m->rank == 0) {
-            const ncclResult_t r = ncclRecv(ptr, bytes, ncclUint8, owner, m->comm, st);
-            if (r != ncclSuccess) {
-                (void)ncclGroupEnd();
-                return set_error(VX_EDEVICE, std::string("ncclRecv failed: ") + ncclGetErrorString(r));
-            }
-        } else if (owner == m->rank) {
-            const ncclResult_t r = ncclSend(ptr, bytes, ncclUint8, 0, m->comm, st);
-            if (r != ncclSuccess) {
-                (void)ncclGroupEnd();
-                return set_error(VX_EDEVICE, std::string("ncclSend failed: ") + ncclGetErrorString(r));
-            }
+    for (const vx_mgpu_xfer &x : xs) {
+        const ncclResult_t r = m->rank == 0 ? ncclRecv(frame + x.offset, x.bytes, ncclUint8, x.src, m->comm, st)
+                                            : ncclSend(frame + x.offset, x.bytes, ncclUint8, x.dst, m->comm, st);
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return set_error(VX_EDEVICE, std::string(m->rank == 0 ? "ncclRecv" : "ncclSend") + " failed: " +
+                                             ncclGetErrorString(r));
         }
     }
     VX_NCCL(ncclGroupEnd());

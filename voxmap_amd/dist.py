@@ -31,6 +31,22 @@ def band_rows_of(b: int, h: int, band_rows: int) -> slice:
     return slice(b * band_rows, min(h, (b + 1) * band_rows))
 
 
+def transfers(w: int, h: int, band_rows: int, world: int, rank: int, pixel_bytes: int) -> list:
+    """The gather's point-to-point moves as ``rank`` issues them (the mirror of
+    vx_mgpu_transfers): (band, src, dst, rows, byte offset, bytes) for every band
+    whose owner is not rank 0 -- all of them on rank 0 (receives), the rank's own
+    elsewhere (sends), in band order."""
+    out = []
+    for b in range(n_bands(h, band_rows)):
+        owner = b % world
+        if owner == 0 or (rank != 0 and owner != rank):
+            continue
+        r = band_rows_of(b, h, band_rows)
+        rows = r.stop - r.start
+        out.append((b, owner, 0, rows, r.start * w * pixel_bytes, rows * w * pixel_bytes))
+    return out
+
+
 class BandGather:
     """One rank's part of a sharded frame: render my bands in place, gather to rank 0.
 
@@ -51,19 +67,20 @@ class BandGather:
         self._render = render_bands
 
     def transfers(self):
-        """(band id, owner) of every band that moves (owner != 0)."""
-        return [(b, b % self.world) for b in range(n_bands(self.h, self.band_rows)) if b % self.world != 0]
+        """This rank's moves of the gather (``transfers``; the native vx_mgpu_transfers)."""
+        px = self.frame.element_size() * self.frame.shape[2]
+        return transfers(self.w, self.h, self.band_rows, self.world, self.rank, px)
 
     def step(self):
         if self.mine:
             self._render(self.mine, self.frame)
         ops = []
-        for b, owner in self.transfers():
+        for b, src, dst, _, _, _ in self.transfers():
             rows = self.frame[band_rows_of(b, self.h, self.band_rows)]
             if self.rank == 0:
-                ops.append(self.dist.P2POp(self.dist.irecv, rows, owner, self.group))
-            elif owner == self.rank:
-                ops.append(self.dist.P2POp(self.dist.isend, rows, 0, self.group))
+                ops.append(self.dist.P2POp(self.dist.irecv, rows, src, self.group))
+            else:
+                ops.append(self.dist.P2POp(self.dist.isend, rows, dst, self.group))
         if ops:
             for req in self.dist.batch_isend_irecv(ops):
                 req.wait()

@@ -254,6 +254,18 @@ def mgpu_bands(h: int, band_rows: int, nranks: int, rank: int) -> list:
     return list(ids[:n])
 
 
+def mgpu_transfers(w: int, h: int, band_rows: int, nranks: int, rank: int, pixel_format: int = 1) -> list:
+    """The gather's transfer list as ``rank`` issues it (vx_mgpu_transfers, a pure
+    host function): [(band, src, dst, rows, byte offset, bytes), ...] in band order."""
+    args = (int(w), int(h), int(band_rows), int(pixel_format), int(nranks), int(rank))
+    n = lib().vx_mgpu_transfers(*args, None, 0)
+    if n < 0:
+        check(n)
+    xs = (_abi.MgpuXfer * max(n, 1))()
+    check(0 if lib().vx_mgpu_transfers(*args, C.cast(xs, C.c_void_p), n) == n else -1)
+    return [(x.band, x.src, x.dst, x.rows, x.offset, x.bytes) for x in xs[:n]]
+
+
 class MultiGPU:
     """One rank of a frame shared by the GPUs of a node (vx_mgpu_*: bands
     rendered in place, gathered into rank 0's frame over RCCL)."""
