@@ -70,6 +70,8 @@ def lib():
         L.vxo_shade.argtypes = [C.POINTER(OScene), C.c_void_p, C.POINTER(OGbuf), C.POINTER(C.c_float),
                                 C.POINTER(C.c_float), C.c_void_p]
         L.vxo_pixel_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+        L.vxo_glass_layers.argtypes = [C.POINTER(OScene), C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.vxo_glass_layers.restype = None
         L.vxo_sun_samples.argtypes = [C.POINTER(C.c_float), C.c_float, C.c_int, C.POINTER(C.c_float)]
         L.vxo_sun_samples.restype = None
         L.vxo_palette.argtypes = [C.POINTER(C.c_float)]
@@ -131,6 +133,12 @@ class Oracle:
         out = (C.c_float * 4)()
         lib().vxo_shade(C.byref(self.sc), C.addressof(params), C.byref(gbuf), (C.c_float * 3)(*prim_dir), out, None)
         return tuple(out)
+
+    def glass_layers(self, params, w: int, h: int, threads: int = 0) -> np.ndarray:
+        """(h, w) uint8: front-facing glass faces in front of each pixel's opaque hit."""
+        out = np.zeros((h, w), np.uint8)
+        lib().vxo_glass_layers(C.byref(self.sc), C.addressof(params), w, h, out.ctypes.data, threads)
+        return out
 
     def pixel_dir(self, params, w, h, px, py):
         d = (C.c_float * 3)()

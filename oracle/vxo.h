@@ -103,6 +103,11 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
 int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float dir[3],
                 vxo_gbuf g[2], int *fetches, int *cap_hit);
 
+/* Diagnostic: per pixel of a w*h frame, the front-facing glass faces the view
+ * ray crosses before its opaque surface (the reference blends each, in draw
+ * order; the build blends the first one: DESIGN.md §5).  out: w*h bytes. */
+void vxo_glass_layers(const vxo_scene *s, const vxo_frame *f, int w, int h, uint8_t *out, int n_threads);
+
 /* Shade one fragment (render.frag:147-252).  out_rgba[3] = alpha. */
 void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
                const float prim_dir[3], float out_rgba[4], vxo_stats *st);

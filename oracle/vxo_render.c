@@ -282,7 +282,7 @@ static inline int in_grid(const vxo_scene *s, const int a[3]) {
  * the next change behind it (primary visibility); 0: the first change ends
  * the walk (reflection rays).  A start cell outside the grid is sky. */
 static int walk(const vxo_scene *s, const int cc[3], const float o[3], const float d[3], int c[3],
-                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit) {
+                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit, int *glass_entries) {
     const int dims[3] = {s->X, s->Y, s->Z};
     float inv[3];
     int stp[3];
@@ -327,6 +327,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
         (*fetches)++;
         const int col = vxo_vis(tx[2]);
         OCT_E(abs_c, E);                           /* air box ahead */
+        if (glass_entries && col == GLASS_INDEX && prev != GLASS_INDEX) (*glass_entries)++;
         /* a front face: entering a meshed cell from a cell of another colour
          * (air is never meshed, sdf.cpp:229-233,284); with glass_layer the
          * first glass entry is recorded and the walk goes on, later glass
@@ -386,7 +387,51 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
         int lo = -cc[i], hi = dims[i] - cc[i] - 1;
         c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
     }
-    return walk(s, cc, o, d, c, 1, g, fetches, cap_hit);
+    return walk(s, cc, o, d, c, 1, g, fetches, cap_hit, NULL);
+}
+
+/* Diagnostic (the single-layer glass deviation): per pixel, the
+ * number of front-facing glass faces the view ray crosses before its opaque
+ * surface or the grid exit -- the glass entries of vxo_primary's walk.  The
+ * reference blends each of them in draw order (render.js:82-86, glass drawn
+ * last, sdf.cpp:284,337); the build blends the first one only, so pixels with
+ * 2 or more are where the two can differ. */
+void vxo_glass_layers(const vxo_scene *s, const vxo_frame *f, int w, int h, uint8_t *out, int n_threads) {
+    (void)n_threads;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int py = 0; py < h; py++)
+        for (int px = 0; px < w; px++) {
+            float d[3];
+            vxo_pixel_dir(f, w, h, px, py, d);
+            const int dims[3] = {s->X, s->Y, s->Z};
+            const float *o = f->cam_fract;
+            const int *cc = f->cam_cell;
+            float tlo = 0.0f, thi = INFINITY;
+            int miss = 0, n = 0;
+            for (int i = 0; i < 3; i++) {
+                float lo = (float)(0 - cc[i]) - o[i], hi = (float)(dims[i] - cc[i]) - o[i];
+                if (d[i] != 0.0f) {
+                    float inv = 1.0f / d[i], t0 = lo * inv, t1 = hi * inv;
+                    if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
+                    tlo = g_max(tlo, t0);
+                    thi = g_min(thi, t1);
+                } else if (!(lo <= 0.0f && 0.0f < hi)) miss = 1;
+            }
+            if (!miss && tlo < thi) {
+                int c[3], fetches = 0, cap = 0;
+                for (int i = 0; i < 3; i++) {
+                    int ci = g_f2i(floorf(o[i] + tlo * d[i]));
+                    int lo = -cc[i], hi = dims[i] - cc[i] - 1;
+                    c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
+                }
+                vxo_gbuf g[2];       /* (the grid boundary has no faces: a glass start cell is no entry) */
+                walk(s, cc, o, d, c, 1, g, &fetches, &cap, &n);
+            }
+            out[(size_t)py * w + px] = (uint8_t)(n > 255 ? 255 : n);
+        }
 }
 
 void vxo_pixel_dir(const vxo_frame *f, int w, int h, int px, int py, float d[3]) {
@@ -667,7 +712,7 @@ static void reflect_color(const shade_ctx *c, const vxo_gbuf *gl, const float rd
     }
     vxo_gbuf h[2];
     int fetches = 0, cap_hit = 0;
-    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit);
+    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit, NULL);
     if (st) { st->reflect_rays++; st->reflect_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
     float rgba[4];
     if (n == 0) {

@@ -138,3 +138,35 @@ def test_hip_primary_only_matches_greedy_mesh(built, case):
     want = vxo_palette()[colour]
     assert np.array_equal(img[ok, :3], want[ok]), int(np.sum(np.any(img[ok, :3] != want[ok], axis=1)))
     assert ok.mean() > 0.99
+
+
+def test_glass_layer_count_matches_the_mesh(built):
+    """The single-layer glass diagnostic (oracle.Oracle.glass_layers)
+    against the restated mesher: two glass panes in front of a wall, seen from
+    outside the grid.  Every non-edge pixel crosses as many front-facing glass
+    quads of the greedy mesh (mesh_ref.cast n_glass) as the walk counts, and the
+    pixels through both panes count 2 -- the pixels where the reference's
+    draw-order blend and the build's one-layer blend can differ."""
+    import oracle
+    import voxmap_amd as vx
+    from oracle import mesh_ref
+    Z, Y, X = 16, 24, 48
+    grid = np.zeros((Z, Y, X), np.uint8)
+    grid[0] = 3                                   # ground
+    grid[1:12, 4:20, 40:42] = 7                   # wall
+    grid[1:12, 4:20, 20] = 21                     # glass pane 1 (x plane 20..21: not a chunk plane)
+    grid[2:10, 6:18, 27] = 21                     # glass pane 2
+    field = vx.field_build(grid)
+    O = oracle.Oracle(field, np.zeros((16, 16, 4), np.uint8))
+    w, h = 64, 48
+    fr = vx.make_frame((-4.0, 12.0, 6.0), (math.pi / 2, 0.0, -math.pi / 2), w, h)
+    p = fr.params
+    n = O.glass_layers(p, w, h).ravel()
+    dirs = np.array([O.pixel_dir(p, w, h, x, y) for y in range(h) for x in range(w)], np.float64)
+    origin = np.array([p.cam_cell[i] + np.float64(p.cam_fract[i]) for i in range(3)])
+    quads = mesh_ref.greedy_mesh(grid)
+    M = mesh_ref.cast(quads, origin, dirs)
+    ok = np.minimum(M["edge_opaque"], M["edge_glass"]) >= 1e-3
+    assert ok.mean() > 0.9
+    assert np.array_equal(n[ok], M["n_glass"][ok]), int(np.sum(n[ok] != M["n_glass"][ok]))
+    assert np.sum(n == 2) > 100 and np.sum(n == 1) > 50

@@ -14,7 +14,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libvoxmap_hip.so")
-SOURCES = ["vx_api.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_mgpu.cpp", "vx_kernels.hip",
+SOURCES = ["vx_api.cpp", "vx_host.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_mgpu.cpp", "vx_kernels.hip",
            "vx_field_gpu.hip"]
 ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
 # -fno-slp-vectorize: packed FP32 (v_pk_*) issues at the cost of two scalar ops

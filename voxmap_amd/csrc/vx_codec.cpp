@@ -7,6 +7,7 @@
 #include <openssl/evp.h>
 #include <zlib.h>
 
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -67,6 +68,8 @@ static int aes_cbc(bool enc, const unsigned char *in, size_t n, const unsigned c
     return VX_OK;
 }
 
+static constexpr size_t kMaxInflate = (size_t)1 << 32;
+
 static int gunzip(const unsigned char *in, size_t n, std::vector<unsigned char> &out, size_t expect) {
     z_stream zs;
     std::memset(&zs, 0, sizeof zs);
@@ -83,6 +86,12 @@ static int gunzip(const unsigned char *in, size_t n, std::vector<unsigned char> 
             if (expect && produced > expect) {
                 inflateEnd(&zs);
                 return set_error(VX_ESIZE, "gzip stream inflates past the expected " + std::to_string(expect) + " bytes");
+            }
+            // an unknown size (vx_decode) is still bounded: no asset of this
+            // path is near 4 GiB (the C5 field is 0.9 GB), a gzip bomb is
+            if (!expect && produced >= kMaxInflate) {
+                inflateEnd(&zs);
+                return set_error(VX_ESIZE, "gzip stream inflates past 4 GiB");
             }
             out.resize(expect && produced == expect ? expect + 1 : out.size() * 2 + 1);
         }
@@ -106,6 +115,9 @@ int decode_container(const unsigned char *in, size_t n, int format, const char *
         out.assign(in, in + n);
         return VX_OK;
     }
+    // zlib counts input in 32 bits and EVP in a signed int: larger inputs are no asset of this path
+    if ((format == VX_FORMAT_BIN_GZ || format == VX_FORMAT_BLOB) && n > (size_t)INT32_MAX)
+        return set_error(VX_ESIZE, "container of " + std::to_string(n) + " bytes is too large");
     if (format == VX_FORMAT_BIN_GZ) return gunzip(in, n, out, expect);
     if (format == VX_FORMAT_BLOB) {
         if (n == 0 || n % 16 != 0)

@@ -11,6 +11,14 @@ namespace vx {
 // Error plumbing: every C entry point returns a VX_E* code and leaves a
 // message in a thread-local buffer (vx_last_error).
 int set_error(int code, const std::string &msg);
+const char *last_error();
+// containers (vx_codec.cpp) and host field / noise builders (vx_field.cpp)
+int decode_container(const unsigned char *in, size_t n, int format, const char *key,
+                     std::vector<unsigned char> &out, size_t expect);
+int format_from_path(const char *path);
+int encrypt_blob(const unsigned char *in, size_t n, const char *key, std::vector<unsigned char> &out);
+int field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba, int n_threads);
+int noise_synth(uint32_t seed, int w, int h, uint8_t *out);
 // the HIP device ordinal a scene lives on (vx_api.cpp)
 int scene_device(const vx_scene *s);
 // the scene's own (non-blocking) stream: what vx_render* run on when given stream == NULL
@@ -117,6 +125,18 @@ struct FieldLayout {
     size_t texels;           // Xp * Yp * Zp, one prim copy
 };
 FieldLayout field_layout(int X, int Y, int Z, int cap);
+
+// vx_scene_create's host half (vx_host.cpp): the description checked, the map
+// and noise containers decoded and size-checked (or the noise synthesised).
+struct SceneInputs {
+    int X = 0, Y = 0, Z = 0, NW = 0, NH = 0, cap = 0;
+    bool from_grid = false;           // VX_FORMAT_GRID: field holds nothing, the device builds it
+    int max_rg = 0;                   // largest R/G of a decoded map.bin (march_pad needs <= Z)
+    std::vector<unsigned char> field, noise;
+};
+int scene_inputs(const vx_scene_desc *d, SceneInputs &in);
+// vx_render*'s frame checks (vx_host.cpp)
+int check_frame(const vx_frame_params *p, int w, int h, int fmt);
 // padded int8 sun channels (border = -1) from the linear RGBA upload
 int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int SB, void *stream);
 // linear RGBA upload -> sun, rg

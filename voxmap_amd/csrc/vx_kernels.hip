@@ -1786,16 +1786,6 @@ __global__ void k_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t
 }
 }  // namespace
 
-FieldLayout field_layout(int X, int Y, int Z, int cap) {
-    FieldLayout L;
-    L.pad = cap;
-    L.Xp = X + 2 * cap;
-    L.Yp = Y + 2 * cap;
-    L.Zp = Z + 2 * cap;
-    L.texels = (size_t)L.Xp * L.Yp * L.Zp;
-    return L;
-}
-
 int launch_field_pack(const uint32_t *lin, uint8_t *sun, uint16_t *rg, int X, int Y, int Z, void *stream) {
     const size_t N = (size_t)X * Y * Z;
     const dim3 grid((unsigned)((N + 255) / 256)), block(256);

@@ -43,43 +43,6 @@ using namespace vx;
 
 extern "C" {
 
-int vx_mgpu_bands(int h, int band_rows, int nranks, int rank, int *ids, int cap) {
-    if (h <= 0 || band_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks)
-        return set_error(VX_EINVAL, "vx_mgpu_bands: bad arguments");
-    const int nb = (h + band_rows - 1) / band_rows;
-    int n = 0;
-    for (int b = rank; b < nb; b += nranks) {
-        if (ids && n < cap) ids[n] = b;
-        n++;
-    }
-    return n;
-}
-
-int vx_mgpu_transfers(int w, int h, int band_rows, int pixel_format, int nranks, int rank, vx_mgpu_xfer *out,
-                      int cap) {
-    if (w <= 0 || h <= 0 || band_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || cap < 0 ||
-        (pixel_format != VX_PIXEL_RGBA8 && pixel_format != VX_PIXEL_RGBA32F))
-        return set_error(VX_EINVAL, "vx_mgpu_transfers: bad arguments");
-    const uint64_t row_bytes = (uint64_t)w * (pixel_format == VX_PIXEL_RGBA32F ? 16u : 4u);
-    const int nb = (h + band_rows - 1) / band_rows;
-    int n = 0;
-    for (int b = 0; b < nb; b++) {
-        const int owner = b % nranks;
-        if (owner == 0 || (rank != 0 && owner != rank)) continue;
-        if (out && n < cap) {
-            vx_mgpu_xfer &x = out[n];
-            x.band = b;
-            x.src = owner;
-            x.dst = 0;
-            x.rows = (b + 1) * band_rows <= h ? band_rows : h - b * band_rows;
-            x.offset = (uint64_t)b * band_rows * row_bytes;
-            x.bytes = (uint64_t)x.rows * row_bytes;
-        }
-        n++;
-    }
-    return n;
-}
-
 int vx_mgpu_unique_id(void *uid) {
     if (!uid) return set_error(VX_EINVAL, "vx_mgpu_unique_id: null argument");
     ncclUniqueId id;
