@@ -30,10 +30,12 @@ struct vx_scene {
     int8_t *d_sunp = nullptr;     // R, G channels, int8, -1 border (Z <= 126)
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
+    uint32_t *d_rg2 = nullptr;    // AO x-pairs: (R, G) of cells x and x + 1, clamped, (X + 1) per row
     uint8_t *d_bcol = nullptr;    // map.bin's B channel as uploaded (vx_scene_read_field)
     uint32_t *d_fp2d = nullptr;   // 2D mode: per column vis colour + quad corner (KernelArgs::fp2d)
     std::vector<Quad2d> quads2d;  // 2D mode: the footprint's greedy quads (vx_scene_vertex2d)
     uint32_t *d_noise = nullptr;
+    uint32_t *d_noise4 = nullptr; // fbm quads: A of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1), wrapped
     unsigned long long *d_stats = nullptr;
     int *d_tiles = nullptr;
     int tiles_cap = 0;
@@ -119,6 +121,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
         (e = hipMalloc(&lin, field_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
+        (e = hipMalloc(&s->d_noise4, noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&s->d_bcol, field_bytes / 4)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
@@ -151,12 +154,15 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
     int *psum = nullptr;   // prefix sums of solid cells for the octant boxes
     if ((e = hipMalloc(&s->d_prim, 8 * L.texels * 4)) == hipSuccess &&
         (e = hipMalloc(&s->d_sun, 2 * N)) == hipSuccess && (e = hipMalloc(&s->d_rg, 2 * N)) == hipSuccess &&
+        (e = hipMalloc(&s->d_rg2, 4 * (N + (size_t)Y * Z))) == hipSuccess &&
         (e = hipMalloc(&psum, sizeof(int) * (size_t)(X + 1) * (Y + 1) * (Z + 1))) == hipSuccess &&
         (e = hipMemsetD32Async((hipDeviceptr_t)s->d_prim, 0xFFFFFFFF, 8 * L.texels, s->stream)) == hipSuccess) {
         // B -> vis colour first: the boxes and prim copies classify by it
         lrc = launch_field_vis(lin, s->d_bcol, X, Y, Z, s->stream);
         if (!lrc) lrc = build_2d(s, lin);
         if (!lrc) lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
+        if (!lrc) lrc = launch_ao_pairs(s->d_rg, s->d_rg2, X, Y, Z, s->stream);
+        if (!lrc) lrc = launch_noise_quads(s->d_noise, s->d_noise4, NW, NH, s->stream);
         if (!lrc) lrc = launch_field_psum(lin, psum, X, Y, Z, s->stream);
         // march copy of the sun channels: int8 inside a border of -1 ("left the grid"), so the
         // march's loaded value carries the exit test (vx_kernels.hip march_fast); values <= Z <= 126
@@ -198,6 +204,8 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_sun) (void)hipFree(s->d_sun);
     if (s->d_sunp) (void)hipFree(s->d_sunp);
     if (s->d_rg) (void)hipFree(s->d_rg);
+    if (s->d_rg2) (void)hipFree(s->d_rg2);
+    if (s->d_noise4) (void)hipFree(s->d_noise4);
     if (s->d_bcol) (void)hipFree(s->d_bcol);
     if (s->d_fp2d) (void)hipFree(s->d_fp2d);
     if (s->d_noise) (void)hipFree(s->d_noise);
@@ -299,7 +307,9 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.SXpYp = (unsigned)s->SXp * (unsigned)s->SYp;
     a.sunp_texels = (unsigned)s->SXp * (unsigned)s->SYp * (unsigned)s->SZp;
     a.rg = s->d_rg;
+    a.rg2 = s->d_rg2;
     a.noise = s->d_noise;
+    a.noise4 = s->d_noise4;
     a.fp2d = s->d_fp2d;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;
     a.noise_w = s->noise_w; a.noise_h = s->noise_h;

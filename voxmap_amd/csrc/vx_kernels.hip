@@ -189,6 +189,7 @@ __device__ __forceinline__ T ld_off(const T *base, unsigned byte_off) {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x3 __attribute__((ext_vector_type(3)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 buf_rsrc(const void *base, unsigned w3) {
     const unsigned long long p = (unsigned long long)base;
     u32x4 r;
@@ -202,15 +203,19 @@ constexpr unsigned kRsrcS8 = 0x0000B004u;  // 8, SSCALED, dst X: the march texel
 constexpr unsigned kRsrcRG = 0x1802Cu;     // 8_8, UNORM, dst (X, Y): (R, G) of a u16 R | G << 8
 constexpr unsigned kRsrcA = 0x50007u;      // 8_8_8_8, UNORM, dst X = W: the A channel
 constexpr unsigned kRsrcRGB = 0x501ACu;    // 8_8_8_8, UNORM, dst (X, Y, Z)
+constexpr unsigned kRsrcRGBA = 0x50FACu;   // 8_8_8_8, UNORM, dst (X, Y, Z, W)
 __device__ float vx_ld_format_f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.f32");
 __device__ f32x2 vx_ld_format_v2f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.v2f32");
 __device__ f32x3 vx_ld_format_v3f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.v3f32");
+__device__ f32x4 vx_ld_format_v4f32(u32x4 rsrc, unsigned voff, int soff, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.format.v4f32");
 __device__ __forceinline__ float ld_fmt1(u32x4 rsrc, unsigned off) { return vx_ld_format_f32(rsrc, off, 0, 0); }
 __device__ __forceinline__ f32x2 ld_fmt2(u32x4 rsrc, unsigned off) { return vx_ld_format_v2f32(rsrc, off, 0, 0); }
 __device__ __forceinline__ f32x3 ld_fmt3(u32x4 rsrc, unsigned off) { return vx_ld_format_v3f32(rsrc, off, 0, 0); }
+__device__ __forceinline__ f32x4 ld_fmt4(u32x4 rsrc, unsigned off) { return vx_ld_format_v4f32(rsrc, off, 0, 0); }
 
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
 __device__ __forceinline__ unsigned lin_index(const KernelArgs &a, int x, int y, int z) {
@@ -703,30 +708,37 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
 }
 
 // sdf(ivec3, vec3) (render.frag:55-58) = min of trilinear R, G at LOD 0.
+// The x-neighbours come in pairs (a.rg2): entry p of a row holds (R, G) of
+// cells clamp(p - 1) and clamp(p), so the lerp's two x corners i0 =
+// clamp(i), i1 = clamp(i + 1) are ONE typed load at p = clamp(i, -1, X - 1) + 1
+// (i <= -1: (0, 0); i >= X - 1: (X - 1, X - 1); else (i, i + 1) -- exactly
+// lin_axis's CLAMP_TO_EDGE pair).  Four 8_8_8_8 UNORM loads per sample
+// instead of eight 8_8 ones, the same RN(b / 255) values, the same lerps.
 __device__ __forceinline__ float sdf_lin(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2) {
     const FrameConsts &F = a.fc;
-    int x0, x1, y0, y1, z0, z1;
+    int y0, y1, z0, z1;
     float wx, wy, wz;
-    lin_axis(((float)c0 + f0) * F.sf[0], a.X, x0, x1, wx);
+    const float ux = ((float)c0 + f0) * F.sf[0] * (float)a.X - 0.5f;
+    const float flx = floorf(ux);
+    wx = ux - flx;
+    const int px = min(max((int)flx, -1), a.X - 1) + 1;     // pair index (AO coordinates are far inside +-2^24)
     lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
     lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
-    // one byte offset and three deltas (0 or one row / plane / cell: the
-    // clamped corners differ by at most one cell per axis)
-    const unsigned b000 = lin_index(a, x0, y0, z0) << 1;
-    const unsigned dx = (unsigned)(x1 - x0) << 1, dy = __umul24((unsigned)(y1 - y0), 2u * (unsigned)a.X),
-                   dz = __umul24((unsigned)(z1 - z0), 2u * a.XY);
-    const unsigned b010 = b000 + dy, b001 = b000 + dz, b011 = b010 + dz;
-    const u32x4 rs = buf_rsrc(a.rg, kRsrcRG);
-    f32x2 u000 = ld_fmt2(rs, b000), u100 = ld_fmt2(rs, b000 + dx), u010 = ld_fmt2(rs, b010);
-    f32x2 u110 = ld_fmt2(rs, b010 + dx), u001 = ld_fmt2(rs, b001), u101 = ld_fmt2(rs, b001 + dx);
-    f32x2 u011 = ld_fmt2(rs, b011), u111 = ld_fmt2(rs, b011 + dx);
+    // one byte offset and two deltas (0 or one row / plane: the clamped corners
+    // differ by at most one cell per axis)
+    const unsigned row = (unsigned)a.X + 1u;
+    const unsigned b00 = ((unsigned)px + __umul24(row, (unsigned)y0) + __umul24(__umul24(row, (unsigned)a.Y), (unsigned)z0)) << 2;
+    const unsigned dy = __umul24((unsigned)(y1 - y0), 4u * row), dz = __umul24((unsigned)(z1 - z0), 4u * row * (unsigned)a.Y);
+    const u32x4 rs = buf_rsrc(a.rg2, kRsrcRGBA);
+    const f32x4 u00 = ld_fmt4(rs, b00), u10 = ld_fmt4(rs, b00 + dy);
+    const f32x4 u01 = ld_fmt4(rs, b00 + dz), u11 = ld_fmt4(rs, b00 + dy + dz);
     float res[2];
 #pragma unroll
     for (int ch = 0; ch < 2; ch++) {
-        const float v00 = gmix(u000[ch], u100[ch], wx);
-        const float v01 = gmix(u010[ch], u110[ch], wx);
-        const float v10 = gmix(u001[ch], u101[ch], wx);
-        const float v11 = gmix(u011[ch], u111[ch], wx);
+        const float v00 = gmix(u00[ch], u00[2 + ch], wx);
+        const float v01 = gmix(u10[ch], u10[2 + ch], wx);
+        const float v10 = gmix(u01[ch], u01[2 + ch], wx);
+        const float v11 = gmix(u11[ch], u11[2 + ch], wx);
         const float w0 = gmix(v00, v01, wy);
         const float w1 = gmix(v10, v11, wy);
         res[ch] = gmix(w0, w1, wz) * 255.0f;
@@ -753,18 +765,18 @@ __device__ __forceinline__ int wrap_idx(float fl, int n) {
 }
 
 // fbm(p) = 1 - 2*texture(u_noise, p).a (render.frag:16-24), bilinear, REPEAT, LOD 0.
+// The four A texels of the bilinear footprint are one typed load from the quad
+// texture a.noise4 (entry (x, y) = A of (x, y), (x+1, y), (x, y+1), (x+1, y+1),
+// REPEAT-wrapped when it was built): the same RN(b / 255) values.
 __device__ __forceinline__ float fbm(const KernelArgs &a, float px, float py) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float wa = u - fu, wb = v - fv;
     const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
-    const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-    const u32x4 rs = buf_rsrc(a.noise, kRsrcA);
-    auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
-    const float t00 = ld_fmt1(rs, off(x0, y0)), t10 = ld_fmt1(rs, off(x1, y0));
-    const float t01 = ld_fmt1(rs, off(x0, y1)), t11 = ld_fmt1(rs, off(x1, y1));
-    const float r0 = gmix(t00, t10, wa), r1 = gmix(t01, t11, wa);
+    const u32x4 rs = buf_rsrc(a.noise4, kRsrcRGBA);
+    const f32x4 t = ld_fmt4(rs, (((unsigned)y0 << a.noise_lw) | (unsigned)x0) << 2);
+    const float r0 = gmix(t.x, t.y, wa), r1 = gmix(t.z, t.w, wa);
     return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
 
@@ -1717,6 +1729,25 @@ __global__ void k_oct_box(const uint32_t *lin, const int *S, uint32_t *dst, int 
     dst[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))] =
         col | ((uint32_t)e[0] << 8) | ((uint32_t)e[1] << 16) | ((uint32_t)e[2] << 24);
 }
+// AO x-pairs (sdf_lin): entry (p, y, z), p = 0..X, = rg of cells clamp(p - 1) and clamp(p)
+__global__ void k_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t row = (size_t)X + 1;
+    if (i >= row * Y * Z) return;
+    const int p = (int)(i % row);
+    const size_t yz = i / row;
+    const int x0 = max(p - 1, 0), x1 = min(p, X - 1);
+    rg2[i] = (uint32_t)rg[yz * X + x0] | ((uint32_t)rg[yz * X + x1] << 16);
+}
+// fbm quads: A of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1) (W, H powers of two, REPEAT)
+__global__ void k_noise_quads(const uint32_t *noise, uint32_t *q, int W, int H) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)W * H) return;
+    const int x = (int)(i % W), y = (int)(i / W);
+    const int x1 = (x + 1) & (W - 1), y1 = (y + 1) & (H - 1);
+    auto A = [&](int xx, int yy) { return noise[(size_t)yy * W + xx] >> 24; };
+    q[i] = A(x, y) | (A(x1, y) << 8) | (A(x, y1) << 16) | (A(x1, y1) << 24);
+}
 // linear RGBA upload -> sun channel arrays and the AO array
 __global__ void k_pack_sun(const uint32_t *src, uint8_t *sun, uint16_t *rg, size_t N) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1785,6 +1816,20 @@ __global__ void k_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t
     dst[i] = (uint32_t)rg[i] | ((uint32_t)bcol[i] << 16) | (r << 24);
 }
 }  // namespace
+
+int launch_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z, void *stream) {
+    const size_t N = ((size_t)X + 1) * Y * Z;
+    hipLaunchKernelGGL(k_ao_pairs, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, rg2, X, Y,
+                       Z);
+    return (int)hipGetLastError();
+}
+
+int launch_noise_quads(const uint32_t *noise, uint32_t *noise4, int W, int H, void *stream) {
+    const size_t N = (size_t)W * H;
+    hipLaunchKernelGGL(k_noise_quads, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, noise,
+                       noise4, W, H);
+    return (int)hipGetLastError();
+}
 
 int launch_field_pack(const uint32_t *lin, uint8_t *sun, uint16_t *rg, int X, int Y, int Z, void *stream) {
     const size_t N = (size_t)X * Y * Z;
