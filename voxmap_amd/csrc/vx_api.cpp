@@ -35,7 +35,7 @@ struct vx_scene {
     uint32_t *d_fp2d = nullptr;   // 2D mode: per column vis colour + quad corner (KernelArgs::fp2d)
     std::vector<Quad2d> quads2d;  // 2D mode: the footprint's greedy quads (vx_scene_vertex2d)
     uint32_t *d_noise = nullptr;
-    uint32_t *d_noise4 = nullptr; // fbm quads: A of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1), wrapped
+    uint32_t *d_noise4 = nullptr; // noise quads, 4 planes (A, R, G, B): a channel of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1), wrapped
     unsigned long long *d_stats = nullptr;
     int *d_tiles = nullptr;
     int tiles_cap = 0;
@@ -121,7 +121,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
         (e = hipMalloc(&lin, field_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_noise, noise_bytes)) != hipSuccess ||
-        (e = hipMalloc(&s->d_noise4, noise_bytes)) != hipSuccess ||
+        (e = hipMalloc(&s->d_noise4, 4 * noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&s->d_bcol, field_bytes / 4)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||

@@ -75,7 +75,8 @@ struct KernelArgs {
     const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *rg2;     // AO x-pairs (X + 1 per row): entry p = (R, G) of cells clamp(p - 1), clamp(p)
     const uint32_t *noise;   // RGBA8 noise texels
-    const uint32_t *noise4;  // fbm quads: entry (x, y) = A of (x, y), (x+1, y), (x, y+1), (x+1, y+1), REPEAT-wrapped
+    const uint32_t *noise4;  // noise quads, planes A, R, G, B: entry (x, y) = that channel of (x, y), (x+1, y),
+                             // (x, y+1), (x+1, y+1), REPEAT-wrapped
     const uint32_t *fp2d;    // 2D mode: 2 words per column (x fastest): vis colour, quad corner x0 | y0 << 16
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
@@ -143,7 +144,7 @@ int check_frame(const vx_frame_params *p, int w, int h, int fmt);
 int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int SB, void *stream);
 // AO x-pair array from rg: (X + 1) * Y * Z u32 (R, G of two x-neighbours, clamped)
 int launch_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z, void *stream);
-// fbm quad texture from the RGBA8 noise (A channel of each texel's 2x2 block, wrapped)
+// noise quad texture from the RGBA8 noise: 4 planes (A, R, G, B) of each texel's wrapped 2x2 block
 int launch_noise_quads(const uint32_t *noise, uint32_t *noise4, int W, int H, void *stream);
 // linear RGBA upload -> sun, rg
 int launch_field_pack(const uint32_t *lin, uint8_t *sun, uint16_t *rg, int X, int Y, int Z, void *stream);

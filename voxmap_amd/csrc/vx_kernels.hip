@@ -57,6 +57,39 @@ __device__ __forceinline__ float div_const(float a, float b, float y) {
     return __builtin_fmaf(r0, y, q0);
 }
 
+// a / b for any sign of a (b > 0, y = RN(1/b)): div_const with the sign of a
+// copied onto the result, so a = -0 gives -0 as the IEEE quotient does.
+// One correction is exact for every pair of significands
+// (tools/micro/markstein_all.hip, profiles/r01_markstein_all.txt), so the
+// divisor may vary per pixel.
+__device__ __forceinline__ float div_shared(float a, float b, float y) {
+    return __builtin_copysignf(div_const(a, b, y), a);
+}
+
+// RN(1/l) for l with |l| in [2^-40, 2^41): v_rcp + one Newton step equals the
+// IEEE reciprocal on every such input (tools/micro/rcp_check.hip, exhaustive
+// over exponents -40..40, both signs: profiles/r01_rcp_check.txt).  Callers
+// guarantee the range.
+__device__ __forceinline__ float rcp_ranged(float l) {
+    const float r = __builtin_amdgcn_rcpf(l);
+    return __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
+}
+
+
+// Correctly rounded sqrt without the wrapper hipcc puts around it.  sqrtf
+// (-fhip-fp32-correctly-rounded-divide-sqrt) is v_sqrt_f32 plus a one-ulp
+// residual correction, wrapped in a 2^32 input scaling for x < 2^-96 and a
+// class test for zero / inf; sqrt_ranged is the correction alone, bit-identical
+// to sqrtf on +-0 and on [2^-96, FLT_MAX] (tools/micro/sqrt_ranged_check.hip,
+// every float of that domain: profiles/r03_sqrt_ranged_check.txt).
+__device__ __forceinline__ float sqrt_ranged(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __uint_as_float(__float_as_uint(s) - 1u), up = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
+    r = __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
+    return r;
+}
+
 // exp2 by the fixed degree-9 polynomial of the numerical contract.
 __device__ __forceinline__ float vexp2(float x) {
     if (x != x) return x;
@@ -187,8 +220,6 @@ __device__ __forceinline__ T ld_off(const T *base, unsigned byte_off) {
 // the waits, schedules independent work under them and never copies or spills
 // a register a load has not written yet.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x3 __attribute__((ext_vector_type(3)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 buf_rsrc(const void *base, unsigned w3) {
     const unsigned long long p = (unsigned long long)base;
@@ -200,21 +231,12 @@ __device__ __forceinline__ u32x4 buf_rsrc(const void *base, unsigned w3) {
     return r;
 }
 constexpr unsigned kRsrcS8 = 0x0000B004u;  // 8, SSCALED, dst X: the march texel
-constexpr unsigned kRsrcRG = 0x1802Cu;     // 8_8, UNORM, dst (X, Y): (R, G) of a u16 R | G << 8
-constexpr unsigned kRsrcA = 0x50007u;      // 8_8_8_8, UNORM, dst X = W: the A channel
-constexpr unsigned kRsrcRGB = 0x501ACu;    // 8_8_8_8, UNORM, dst (X, Y, Z)
-constexpr unsigned kRsrcRGBA = 0x50FACu;   // 8_8_8_8, UNORM, dst (X, Y, Z, W)
+constexpr unsigned kRsrcRGBA = 0x50FACu;   // 8_8_8_8, UNORM, dst (X, Y, Z, W): AO pairs, noise quads
 __device__ float vx_ld_format_f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.f32");
-__device__ f32x2 vx_ld_format_v2f32(u32x4 rsrc, unsigned voff, int soff, int aux)
-    __asm("llvm.amdgcn.raw.buffer.load.format.v2f32");
-__device__ f32x3 vx_ld_format_v3f32(u32x4 rsrc, unsigned voff, int soff, int aux)
-    __asm("llvm.amdgcn.raw.buffer.load.format.v3f32");
 __device__ f32x4 vx_ld_format_v4f32(u32x4 rsrc, unsigned voff, int soff, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.format.v4f32");
 __device__ __forceinline__ float ld_fmt1(u32x4 rsrc, unsigned off) { return vx_ld_format_f32(rsrc, off, 0, 0); }
-__device__ __forceinline__ f32x2 ld_fmt2(u32x4 rsrc, unsigned off) { return vx_ld_format_v2f32(rsrc, off, 0, 0); }
-__device__ __forceinline__ f32x3 ld_fmt3(u32x4 rsrc, unsigned off) { return vx_ld_format_v3f32(rsrc, off, 0, 0); }
 __device__ __forceinline__ f32x4 ld_fmt4(u32x4 rsrc, unsigned off) { return vx_ld_format_v4f32(rsrc, off, 0, 0); }
 
 // x + X*y + XY*z; X*Y < 2^23 (vx_scene_create): full-rate 24-bit multiplies
@@ -780,27 +802,9 @@ __device__ __forceinline__ float fbm(const KernelArgs &a, float px, float py) {
     return 1.0f - 2.0f * gmix(r0, r1, wb);
 }
 
-// a / b for any sign of a (b > 0, y = RN(1/b)): div_const with the sign of a
-// copied onto the result, so a = -0 gives -0 as the IEEE quotient does.
-// One correction is exact for every pair of significands
-// (tools/micro/markstein_all.hip, profiles/r01_markstein_all.txt), so the
-// divisor may vary per pixel.
-__device__ __forceinline__ float div_shared(float a, float b, float y) {
-    return __builtin_copysignf(div_const(a, b, y), a);
-}
-
-// RN(1/l) for l with |l| in [2^-40, 2^41): v_rcp + one Newton step equals the
-// IEEE reciprocal on every such input (tools/micro/rcp_check.hip, exhaustive
-// over exponents -40..40, both signs: profiles/r01_rcp_check.txt).  Callers
-// guarantee the range.
-__device__ __forceinline__ float rcp_ranged(float l) {
-    const float r = __builtin_amdgcn_rcpf(l);
-    return __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
-}
-
 // normalize3 of a vector whose length lies in [2^-40, 2^41) (exactly the IEEE result)
 __device__ __forceinline__ void normalize3_ranged(float v0, float v1, float v2, float &o0, float &o1, float &o2) {
-    const float l = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    const float l = sqrt_ranged(v0 * v0 + v1 * v1 + v2 * v2);   // callers: |v|^2 in [2^-80, 2^82)
     const float y = rcp_ranged(l);
     o0 = div_shared(v0, l, y); o1 = div_shared(v1, l, y); o2 = div_shared(v2, l, y);
 }
@@ -837,10 +841,10 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, float d0, float d
     }
     cnt.noise_px++;
     const float ct = F.cloudTime;
-    const float den = sqrtf(fabsf(r2) + 0.03f);
+    const float den = sqrt_ranged(fabsf(r2) + 0.03f);   // in [0.03, 1.03]
     float sx, sy;                                                                 // :184
     {
-        const float y = 1.0f / den;
+        const float y = rcp_ranged(den);    // den = sqrt(|r2| + 0.03) in [0.17, 1.02]
         sx = div_shared(r0, den, y); sy = div_shared(r1, den, y);
     }
     sx = sx * 0.1f; sy = sy * 0.1f;
@@ -871,25 +875,19 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, float d0, float d
 
 // ---------------- extensions (DESIGN.md §3 "Extensions") ----------------
 // white(p) = 1 - 2*texture(u_noise, p).rgb (render.frag:16-21), bilinear REPEAT LOD 0.
+// The bilinear footprint's four texels of each channel are one typed load
+// from that channel's plane of the quad texture (a.noise4 planes 1..3).
 __device__ __forceinline__ void white(const KernelArgs &a, float px, float py, float &w0, float &w1, float &w2) {
     const int W = a.noise_w, H = a.noise_h;
     const float u = px * (float)W - 0.5f, v = py * (float)H - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float wa = u - fu, wb = v - fv;
     const int x0 = wrap_idx(fu, W), y0 = wrap_idx(fv, H);
-    const int x1 = (x0 + 1) & (W - 1), y1 = (y0 + 1) & (H - 1);
-    float w[3];
-    const u32x4 rs = buf_rsrc(a.noise, kRsrcRGB);
-    auto off = [&](int x, int y) { return (((unsigned)y << a.noise_lw) | (unsigned)x) << 2; };
-    f32x3 u00 = ld_fmt3(rs, off(x0, y0)), u10 = ld_fmt3(rs, off(x1, y0));
-    f32x3 u01 = ld_fmt3(rs, off(x0, y1)), u11 = ld_fmt3(rs, off(x1, y1));
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) {
-        const float r0 = gmix(u00[ch], u10[ch], wa);
-        const float r1 = gmix(u01[ch], u11[ch], wa);
-        w[ch] = 1.0f - 2.0f * gmix(r0, r1, wb);
-    }
-    w0 = w[0]; w1 = w[1]; w2 = w[2];
+    const unsigned off = (((unsigned)y0 << a.noise_lw) | (unsigned)x0) << 2, plane = ((unsigned)W * (unsigned)H) << 2;
+    const u32x4 rs = buf_rsrc(a.noise4, kRsrcRGBA);
+    const f32x4 tr = ld_fmt4(rs, off + plane), tg = ld_fmt4(rs, off + 2u * plane), tb = ld_fmt4(rs, off + 3u * plane);
+    auto bil = [&](const f32x4 &t) { return 1.0f - 2.0f * gmix(gmix(t.x, t.y, wa), gmix(t.z, t.w, wa), wb); };
+    w0 = bil(tr); w1 = bil(tg); w2 = bil(tb);
 }
 
 constexpr float kRoughScale = 0.00390625f;   // 1/256: 4 noise texels per voxel
@@ -1739,14 +1737,23 @@ __global__ void k_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int 
     const int x0 = max(p - 1, 0), x1 = min(p, X - 1);
     rg2[i] = (uint32_t)rg[yz * X + x0] | ((uint32_t)rg[yz * X + x1] << 16);
 }
-// fbm quads: A of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1) (W, H powers of two, REPEAT)
+// noise quads: per texel (x, y), one u32 per channel plane holding that channel
+// of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1) (W, H powers of two, REPEAT):
+// plane 0 = A (fbm), planes 1..3 = R, G, B (white)
 __global__ void k_noise_quads(const uint32_t *noise, uint32_t *q, int W, int H) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)W * H) return;
+    const size_t n = (size_t)W * H;
+    if (i >= n) return;
     const int x = (int)(i % W), y = (int)(i / W);
     const int x1 = (x + 1) & (W - 1), y1 = (y + 1) & (H - 1);
-    auto A = [&](int xx, int yy) { return noise[(size_t)yy * W + xx] >> 24; };
-    q[i] = A(x, y) | (A(x1, y) << 8) | (A(x, y1) << 16) | (A(x1, y1) << 24);
+    const uint32_t t00 = noise[(size_t)y * W + x], t10 = noise[(size_t)y * W + x1];
+    const uint32_t t01 = noise[(size_t)y1 * W + x], t11 = noise[(size_t)y1 * W + x1];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const int sh = p == 0 ? 24 : 8 * (p - 1);
+        q[p * n + i] = ((t00 >> sh) & 0xffu) | (((t10 >> sh) & 0xffu) << 8) | (((t01 >> sh) & 0xffu) << 16) |
+                       (((t11 >> sh) & 0xffu) << 24);
+    }
 }
 // linear RGBA upload -> sun channel arrays and the AO array
 __global__ void k_pack_sun(const uint32_t *src, uint8_t *sun, uint16_t *rg, size_t N) {
