@@ -246,6 +246,17 @@ def fps_with_d2h(torch, vx, scene, frame, W, H, frames, K=2):
                    "overlapped with the next frame's render"}
 
 
+def bound_of(pmc):
+    """The unit that measurably binds the kernel, from the committed PMC summary:
+    VALU issue (valu_busy is a lower bound: 2 cycles per instruction) or the CU's
+    texture address / data path (TA / TD busy, one per CU for its 4 SIMDs); the
+    field is cache-resident, so HBM is never it (roofline.traffic << algorithmic)."""
+    if not pmc:
+        return "hbm"
+    td = max(pmc.get("ta_busy") or 0.0, pmc.get("td_busy") or 0.0)
+    return "texture path (TA/TD)" if td > (pmc.get("valu_busy") or 0.0) + 0.1 else "valu"
+
+
 def roofline_of(alg_bytes, ms):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
     return achieved, achieved / HBM_PEAK_GBPS
@@ -572,7 +583,7 @@ def main(argv=None):
                 # that measurably binds the kernel: VALU issue (valu block: rocprofv3 PMC
                 # kept under profiles/), the field being cache-resident (traffic = fabric
                 # bytes << algorithmic)
-                "bound": "valu" if valu else "hbm",
+                "bound": bound_of(valu),
                 "kernel": "k_render (fused primary visibility + shading + sun march" +
                           (" + reflection walk" if flags & vx.FLAG_REFLECT else "") + ")",
                 "achieved": round(achieved, 2),
@@ -586,6 +597,8 @@ def main(argv=None):
                                 if traffic else None),
                 "valu": ({k: valu[k] for k in ("valu_busy", "valu_lane_util", "valu_insts_per_wave", "clock_ghz",
                                                "source") if k in valu} if valu else None),
+                "texture_path": ({k: valu[k] for k in ("ta_busy", "td_busy") if valu.get(k) is not None}
+                                 if valu else None),
             },
         }
         if standin:

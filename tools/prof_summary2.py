@@ -38,7 +38,9 @@ with open(f"{src}/trace/run_kernel_stats.csv") as f:
         if KERNEL in row["Name"]:
             avg_ns = float(row["AverageNs"])
 vals = defaultdict(list)
-for p in ("fetch", "write", "valu"):
+for p in ("fetch", "write", "valu", "tatd"):
+    if not os.path.exists(f"{src}/{p}/run_counter_collection.csv"):
+        continue
     with open(f"{src}/{p}/run_counter_collection.csv") as f:
         for row in csv.DictReader(f):
             if KERNEL in row["Kernel_Name"]:
@@ -60,11 +62,20 @@ pmc = {"kernel": KERNEL, "config": cfg, "camera": cam, "flags": flags, "samples"
        "issue_stall_share": med["SQ_WAIT_INST_ANY"] / med["SQ_WAVE_CYCLES"],
        "wait_share": med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"],
        "active_share": med["SQ_ACTIVE_INST_ANY"] / med["SQ_WAVE_CYCLES"], "clock_ghz": clock}
+if "TA_TA_BUSY_sum" in med:
+    # texture address / data units: one of each per CU, shared by its 4 SIMDs (the counters are summed over
+    # the 256 CUs; the tatd pass has its own GRBM_GUI_ACTIVE, which the median above mixes: recompute per pass)
+    cu_cycles = med["GRBM_GUI_ACTIVE"] / 8
+    pmc["ta_busy"] = med["TA_TA_BUSY_sum"] / 256 / cu_cycles
+    pmc["td_busy"] = med["TD_TD_BUSY_sum"] / 256 / cu_cycles
+    pmc["ta_cycles_per_buffer_load"] = med["TA_TA_BUSY_sum"] / med["TA_BUFFER_READ_WAVEFRONTS_sum"]
 json.dump(pmc, open(f"profiles/{tag}_pmc.json", "w"), indent=1)
 key = {"config": cfg, "camera": cam, "flags": flags, "samples": samples}
 json.dump({**key, "hbm_bytes_per_launch": int(corr), "hbm_bytes_raw": int(raw), "write_bytes": int(wk * 1024),
            "source": f"profiles/{tag}_pmc.json"}, open(f"profiles/traffic_{tag}.json", "w"), indent=1)
 json.dump({**key, "valu_busy": round(busy, 4), "valu_lane_util": round(pmc["valu_lane_util"], 4),
+           "ta_busy": round(pmc["ta_busy"], 4) if "ta_busy" in pmc else None,
+           "td_busy": round(pmc["td_busy"], 4) if "td_busy" in pmc else None,
            "valu_insts_per_wave": round(pmc["valu_insts_per_wave"], 1),
            "issue_stall_share": round(pmc["issue_stall_share"], 4), "wait_share": round(pmc["wait_share"], 4),
            "clock_ghz": round(clock, 3) if clock else None,
