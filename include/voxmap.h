@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 6
+#define VX_ABI_VERSION 7
 
 /* error codes */
 #define VX_OK 0
@@ -88,6 +88,13 @@ extern "C" {
  * around each fragment staged per pass; DESIGN.md §6 "C5").  Identical frames;
  * an experiment, off by default (slower on C5). */
 #define VX_FLAG_SOFT_BRICK 0x100u
+/* Diagnostics: march without the sun exit tables (DESIGN.md §3 "Sun exit
+ * tables"), i.e. every step render.frag:92-136 takes.  Identical frames; the
+ * shadow fetch counters are the reference's own step counts instead of the
+ * steps this build takes. */
+#define VX_FLAG_NO_EXIT 0x200u
+/* Diagnostics: the orthant exit tables only, no per-sun cone table.  Identical frames. */
+#define VX_FLAG_NO_CONE 0x400u
 #define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;
@@ -192,6 +199,24 @@ int vx_render(vx_scene *scene, const vx_frame_params *p, int w, int h, int pixel
 int vx_render_tiles(vx_scene *scene, const vx_frame_params *p, int w, int h, int tile_size,
                     const int *tile_ids, int n_tiles, int pixel_format, void *out_device,
                     void *stream, vx_stats *stats);
+
+/* Sun exit tables (ABI 7; DESIGN.md §3 "Sun exit tables").  The sun march
+ * reads a copy of the march channel in which every cell from which the march
+ * cannot end unlit holds the "left the grid" mark, so a march stops there,
+ * lit, instead of stepping on to the grid edge (render.frag:92-136): the same
+ * lit flag on every pixel, fewer steps.  Orthant copies (valid for any sun of
+ * their octant) are built with the scene; a cone copy for the frame's sun
+ * samples {octant, kx, ky} is built by the first vx_render* that needs it
+ * (stream-ordered; the scene keeps two) -- the sun moves slowly
+ * (map.js:399-402), so one copy serves many frames.  vx_prepare_sun builds the
+ * copy frame p will read ahead of time (when the sun moves, off a frame's
+ * path) and reports which one it is: kind 0 = none (a sun component below
+ * 2^-10, a field without the padded march copy, or VX_FLAG_NO_EXIT), 1 = the
+ * orthant copies, 2 = a cone copy. */
+typedef struct vx_exit_info {
+    int kind, octant, kx, ky;
+} vx_exit_info;
+int vx_prepare_sun(vx_scene *scene, const vx_frame_params *p, void *stream, vx_exit_info *info);
 
 /* Scatter a compact tile-major device buffer back into a w*h frame. */
 int vx_detile(vx_scene *scene, int w, int h, int tile_size, const int *tile_ids, int n_tiles,

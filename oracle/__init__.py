@@ -22,7 +22,8 @@ LIB_PATH = os.path.join(_HERE, "build", "libvxo.so")
 
 class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
-                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p)]
+                ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p),
+                ("exit_mode", C.c_int)]
 
 
 class OStats(C.Structure):
@@ -81,6 +82,11 @@ def lib():
         L.vxo_field_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vxo_field_octant.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vxo_field_box.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.vxo_field_exit.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.vxo_field_exit.restype = None
+        L.vxo_exit_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_int)]
+        L.vxo_exit_plan.restype = C.c_int
         _lib = L
     return _lib
 
@@ -88,7 +94,14 @@ def lib():
 class Oracle:
     """Scalar restatement of render.frag over one field + noise texture."""
 
-    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_e=None):
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_e=None, exit=False):
+        """exit=False: the reference's literal march (every step of
+        render.frag:92-136 counted).  exit=True: the build's sun exit tables
+        (field_exit, chosen per frame by exit_plan) where the HIP kernel has
+        them -- fields with Z <= 126 and every R, G <= Z (its padded int8 march
+        copies) -- so the shadow fetch counters match the kernel's;
+        exit="orthant": the orthant tables only (the kernel's VX_FLAG_NO_CONE).
+        Frames are identical in every mode."""
         self.field = np.ascontiguousarray(field_zyx4, np.uint8)
         self.noise = np.ascontiguousarray(noise_hw4, np.uint8)
         Z, Y, X, _ = self.field.shape
@@ -103,8 +116,11 @@ class Oracle:
         for e in self.oct_e:
             assert e.shape == (Z, Y, X, 3)
         self.fp2d = footprint_2d(self.field)
+        mode = 0
+        if exit and Z <= 126 and int(self.field[..., :2].max(initial=0)) <= Z:
+            mode = 2 if exit == "orthant" else 1
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
-                         (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data)
+                         (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data, mode)
 
     def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
         """RGBA fp32 (h, w, 4); rows not in (row0::row_step) are NaN."""
@@ -203,6 +219,28 @@ def field_box(field_zyx4: np.ndarray, oct: int, cap: int = 32, r_cube=None) -> n
     out = np.empty((Z, Y, X, 3), np.uint8)
     lib().vxo_field_box(f.ctypes.data, X, Y, Z, cap, oct, r.ctypes.data, out.ctypes.data)
     return out
+
+
+def field_exit(field_zyx4: np.ndarray, oct: int, kx: int = -1, ky: int = -1) -> np.ndarray:
+    """(Z, Y, X) uint8: the sun exit table (vxo_field_exit) for
+    sun octant ``oct`` (bit i: r_i > 0) and window (kx, ky); -1 = unbounded,
+    the orthant table.  1 marks a cell from which the march cannot end unlit."""
+    f = np.ascontiguousarray(field_zyx4, np.uint8)
+    Z, Y, X, _ = f.shape
+    out = np.empty((Z, Y, X), np.uint8)
+    lib().vxo_field_exit(f.ctypes.data, X, Y, Z, oct, kx, ky, out.ctypes.data)
+    return out
+
+
+def exit_plan(dirs, allow_cone: bool = True):
+    """(cone, [octant per sample or -1], kx, ky): the build's table choice for
+    a frame's sun directions (vxo_exit_plan)."""
+    d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
+    n = d.shape[0]
+    oct = (C.c_int * n)()
+    kx, ky = C.c_int(), C.c_int()
+    cone = lib().vxo_exit_plan(d.ctypes.data, n, int(allow_cone), oct, C.byref(kx), C.byref(ky))
+    return bool(cone), list(oct), kx.value, ky.value
 
 
 def sun_samples(sun, radius: float, n: int) -> np.ndarray:

@@ -39,6 +39,10 @@ typedef struct {
     const uint8_t *oct_e[8];  /* vxo_field_box per ray octant: 3 extents per cell (primary traversal) */
     const uint32_t *fp2d;     /* 2D mode (quality 0): per column (x fastest) colour, quad corner x0 | y0 << 16
                                  of the sdf.cpp:362-401 mesh (oracle/__init__.py footprint_2d); may be NULL */
+    int exit_mode;            /* 0: the reference's literal march, every step of render.frag:92-136 counted.
+                                 1: the build's sun exit tables (vxo_field_exit, chosen per frame by
+                                 vxo_exit_plan), so the shadow fetch counters equal the kernel's; frames are
+                                 identical either way.  2: orthant tables only (VX_FLAG_NO_CONE). */
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */
@@ -155,6 +159,16 @@ void vxo_field_octant(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct
  * (0, 0, 0) for non-air cells.  3*X*Y*Z bytes into e_out, x fastest. */
 void vxo_field_box(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, const uint8_t *r_cube,
                    uint8_t *e_out);
+/* Sun exit table for sun octant oct (bit i: r_i > 0) and window (kx, ky) (< 0:
+ * unbounded, the orthant table): out[c] = 1 marks a cell from which the march
+ * cannot end unlit.  X*Y*Z bytes, x fastest; definition in vxo_field.c. */
+void vxo_field_exit(const uint8_t *rgba, int X, int Y, int Z, int oct, int kx, int ky, uint8_t *out);
+/* Which exit table a frame's sun march reads (the build's rule):
+ * sample k of n (directions dirs[k]) uses table {oct[k], kx, ky}, or none
+ * (oct[k] = -1: the literal path, some |r_i| < 2^-10).  Returns 1 when every
+ * sample shares one cone table (kx, ky >= 0), else 0 (orthant tables, kx = ky
+ * = -1).  allow_cone = 0 forces the orthant tables. */
+int vxo_exit_plan(const float dirs[][3], int n, int allow_cone, int oct[], int *kx, int *ky);
 
 #ifdef __cplusplus
 }

@@ -226,3 +226,55 @@ void vxo_field_box(const uint8_t *rgba, int X, int Y, int Z, int cap, int oct, c
             }
     free(S);
 }
+
+/* Exit table of the build's sun march (DESIGN.md §3 "Sun exit tables") for
+ * sun octant oct (bit i: r_i > 0) and the channel the march reads for it (R
+ * if r_z > 0, else G: render.frag:47-50, 89).  out[c] = 1 marks a cell from
+ * which the march cannot end unlit: it can only leave the grid or run out of
+ * steps, "lit" either way (render.frag:123-126, 234).  Layer recursion along
+ * z, from the far end in the ray's z direction:
+ *   D(x, y, z) = AND over i = 0..kx, j = 0..ky of
+ *                [T(x', y', z) != 0 and D(x', y', z + sz)],  x' = x + i*sx, y' = y + j*sy,
+ * cells outside the grid counting as true (D beyond the last layer = true).
+ * kx, ky < 0 mean unbounded (every x' from x to the grid edge): D(c) = "no 0
+ * texel in the orthant ahead of c" -- valid for every direction of the
+ * octant.  kx = ceil(max |r_x / r_z| + 1/64) (ky likewise) bounds the cells a
+ * ray crossing one z layer can touch from any point of c: valid for every
+ * direction of the octant with those slopes (the cone tables).  Why this is
+ * exact is DESIGN.md §3; this is the definition the kernel's tables must equal.
+ * Each layer: B = [T != 0] and D(next layer); R = the window AND of B along
+ * x, D = the window AND of R along y, both from run lengths of trues counted
+ * from the far end of the ray's side. */
+void vxo_field_exit(const uint8_t *rgba, int X, int Y, int Z, int oct, int kx, int ky, uint8_t *out) {
+    const int sx = (oct & 1) ? 1 : -1, sy = (oct & 2) ? 1 : -1, sz = (oct & 4) ? 1 : -1;
+    const int ch = sz > 0 ? 0 : 1;
+    const size_t XY = (size_t)X * Y;
+    uint8_t *B = (uint8_t *)malloc(XY), *R = (uint8_t *)malloc(XY);
+    int *run = (int *)malloc(sizeof(int) * (size_t)(X > Y ? X : Y));
+    const int INF = 1 << 30;
+    for (int k = 0; k < Z; k++) {
+        const int z = sz > 0 ? Z - 1 - k : k;
+        const uint8_t *prev = k ? out + (size_t)(z + sz) * XY : NULL;
+        for (size_t j = 0; j < XY; j++)
+            B[j] = rgba[4 * ((size_t)z * XY + j) + ch] != 0 && (!prev || prev[j]);
+        /* R(x, y) = B true on x' = x, x + sx, ..., x + kx*sx (inside the grid) */
+        for (int y = 0; y < Y; y++) {
+            const uint8_t *b = B + (size_t)y * X;
+            for (int t = 0; t < X; t++) {
+                const int x = sx > 0 ? X - 1 - t : t;   /* from the far end */
+                run[x] = !b[x] ? 0 : (t == 0 ? INF : (run[x + sx] >= INF ? INF : run[x + sx] + 1));
+            }
+            for (int x = 0; x < X; x++) R[(size_t)y * X + x] = run[x] >= INF || (kx >= 0 && run[x] > kx);
+        }
+        /* D(x, y) = R true on y' = y, ..., y + ky*sy */
+        uint8_t *d = out + (size_t)z * XY;
+        for (int x = 0; x < X; x++) {
+            for (int t = 0; t < Y; t++) {
+                const int y = sy > 0 ? Y - 1 - t : t;
+                run[y] = !R[(size_t)y * X + x] ? 0 : (t == 0 ? INF : (run[y + sy] >= INF ? INF : run[y + sy] + 1));
+            }
+            for (int y = 0; y < Y; y++) d[(size_t)y * X + x] = run[y] >= INF || (ky >= 0 && run[y] > ky);
+        }
+    }
+    free(B); free(R); free(run);
+}

@@ -18,6 +18,7 @@
  */
 #include "vxo.h"
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -204,8 +205,11 @@ static void white(const vxo_scene *s, float px, float py, float out[3]) {
 }
 
 /* ---------------- march() (render.frag:75-142), literally ---------------- */
-void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
-               const float r[3], int max_steps, vxo_march_t *res) {
+/* ex: the build's exit table for this direction (vxo_exit_plan), or NULL for
+ * the reference's literal march.  A march entering a flagged cell ends "lit"
+ * without fetching it, as the kernel's march does on the -1 its table holds. */
+static void march_ex(const vxo_scene *s, const int cell[3], const float fract[3],
+                     const float r[3], int max_steps, vxo_march_t *res, const uint8_t *ex) {
     res->step = 0;
     res->fetches = 0;
     res->cell[0] = cell[0]; res->cell[1] = cell[1]; res->cell[2] = cell[2];
@@ -236,6 +240,10 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
             res->step = max_steps;
             break;
         }
+        if (ex && ex[(size_t)res->cell[0] + (size_t)s->X * ((size_t)res->cell[1] + (size_t)s->Y * res->cell[2])]) {
+            res->step = max_steps;                       /* exit table: lit, no fetch */
+            break;
+        }
         float rgb[3];
         tex_fetch(s, res->cell, rgb);                                                   /* :128 */
         res->fetches++;
@@ -243,6 +251,40 @@ void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
         res->step++;                                                                    /* :135 */
     }
     for (int i = 0; i < 3; i++) res->normal[i] = -g_sign(r[i] * m[i]);                /* :139 */
+}
+
+void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
+               const float r[3], int max_steps, vxo_march_t *res) {
+    march_ex(s, cell, fract, r, max_steps, res, NULL);
+}
+
+/* The build's choice of exit table per sample (DESIGN.md §3 "Sun exit
+ * tables"), restated: a sample with some |r_i| < 2^-10 takes the literal path
+ * (no table).  If every sample is on the fast path with one sign pattern,
+ * r_z > 0 and slopes |r_x / r_z|, |r_y / r_z| <= 4 (double), all share the cone
+ * table kx = ceil(max |r_x / r_z| + 1/64), ky likewise; otherwise each fast
+ * sample reads the orthant table of its own octant. */
+int vxo_exit_plan(const float dirs[][3], int n, int allow_cone, int oct[], int *kx, int *ky) {
+    const float lim = 0.0009765625f;
+    int all_fast = 1, same = 1;
+    double ax = 0.0, ay = 0.0;
+    for (int k = 0; k < n; k++) {
+        const float *r = dirs[k];
+        const int fast = fabsf(r[0]) >= lim && fabsf(r[1]) >= lim && fabsf(r[2]) >= lim;
+        oct[k] = fast ? ((r[0] > 0.0f ? 1 : 0) | (r[1] > 0.0f ? 2 : 0) | (r[2] > 0.0f ? 4 : 0)) : -1;
+        all_fast &= fast;
+        if (k && oct[k] != oct[0]) same = 0;
+        if (fast) {
+            const double sx = fabs((double)r[0] / (double)r[2]), sy = fabs((double)r[1] / (double)r[2]);
+            ax = sx > ax ? sx : ax;
+            ay = sy > ay ? sy : ay;
+        }
+    }
+    *kx = *ky = -1;
+    if (!allow_cone || !all_fast || !same || !(oct[0] & 4) || ax > 4.0 || ay > 4.0) return 0;
+    *kx = (int)ceil(ax + 1.0 / 64.0);
+    *ky = (int)ceil(ay + 1.0 / 64.0);
+    return 1;
 }
 
 /* ---------------- primary visibility ----------------
@@ -517,6 +559,9 @@ typedef struct {
     int max_steps;
     int n_sun;                               /* >= 2: soft shadows */
     float sun_dirs[VXO_MAX_SAMPLES][3];
+    const uint8_t *ex[VXO_MAX_SAMPLES];      /* exit table per sample (exit_mode), else NULL */
+    uint8_t *owned[VXO_MAX_SAMPLES];
+    int n_owned;
 } shade_ctx;
 
 static void ctx_init(shade_ctx *c, const vxo_scene *s, const vxo_frame *f) {
@@ -525,6 +570,36 @@ static void ctx_init(shade_ctx *c, const vxo_scene *s, const vxo_frame *f) {
     c->max_steps = f->max_shadow_steps > 0 ? f->max_shadow_steps : 2 * s->Z;
     c->n_sun = f->shadow_samples > 1 ? (f->shadow_samples > VXO_MAX_SAMPLES ? VXO_MAX_SAMPLES : f->shadow_samples) : 1;
     vxo_sun_samples(f->sun_dir, f->sun_radius, c->n_sun, c->sun_dirs);
+    c->n_owned = 0;
+    for (int k = 0; k < VXO_MAX_SAMPLES; k++) c->ex[k] = NULL;
+}
+
+/* the frame's exit tables (vxo_render only: a table is a pass over the field) */
+static void ctx_tables(shade_ctx *c) {
+    const vxo_scene *s = c->s;
+    if (!s->exit_mode) return;
+    int oct[VXO_MAX_SAMPLES], kx, ky, key[VXO_MAX_SAMPLES];
+    /* the kernel's cone copies need Z >= 3 (their window inside its -1 border) */
+    vxo_exit_plan((const float(*)[3])c->sun_dirs, c->n_sun, s->exit_mode == 1 && s->Z >= 3, oct, &kx, &ky);
+    for (int k = 0; k < c->n_sun; k++) {
+        if (oct[k] < 0) continue;
+        int found = -1;
+        for (int j = 0; j < c->n_owned; j++)
+            if (key[j] == oct[k]) found = j;
+        if (found < 0) {
+            uint8_t *t = (uint8_t *)malloc((size_t)s->X * s->Y * s->Z);
+            vxo_field_exit(s->field, s->X, s->Y, s->Z, oct[k], kx, ky, t);
+            key[c->n_owned] = oct[k];
+            c->owned[c->n_owned] = t;
+            found = c->n_owned++;
+        }
+        c->ex[k] = c->owned[found];
+    }
+}
+
+static void ctx_free(shade_ctx *c) {
+    for (int j = 0; j < c->n_owned; j++) free(c->owned[j]);
+    c->n_owned = 0;
 }
 
 /* ---------------- main() (render.frag:147-252) ----------------
@@ -648,13 +723,13 @@ static void shade_frag(const shade_ctx *c, const vxo_gbuf *g, const float ray[3]
     if (shadeFactor > 0.0f && !(f->flags & 0x1u)) {  /* :232; VX_FLAG_NO_SHADOW skips */
         vxo_march_t sun;
         if (c->n_sun <= 1) {
-            vxo_march(s, g->cell, g->fract, sunDir, c->max_steps, &sun);            /* :233 */
+            march_ex(s, g->cell, g->fract, sunDir, c->max_steps, &sun, c->ex[0]);   /* :233 */
             shadeFactor = shadeFactor * (sun.step == c->max_steps ? 1.0f : 0.0f);   /* :234 */
             if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
         } else {                 /* ext soft shadows: lit fraction of the sun samples */
             int lit = 0;
             for (int k = 0; k < c->n_sun; k++) {
-                vxo_march(s, g->cell, g->fract, c->sun_dirs[k], c->max_steps, &sun);
+                march_ex(s, g->cell, g->fract, c->sun_dirs[k], c->max_steps, &sun, c->ex[k]);
                 lit += sun.step == c->max_steps ? 1 : 0;
                 if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
             }
@@ -846,6 +921,7 @@ void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
     int nrows = row0 < h ? (h - 1 - row0) / row_step + 1 : 0;
     shade_ctx ctx;
     ctx_init(&ctx, s, f);
+    ctx_tables(&ctx);
     vxo_stats acc;
     memset(&acc, 0, sizeof acc);
 #ifdef _OPENMP
@@ -872,5 +948,6 @@ void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
         }
     }
     if (st) *st = acc;
+    ctx_free(&ctx);
     (void)n_threads;
 }

@@ -48,6 +48,34 @@ def test_oracle_reproduces_golden(built, case):
     assert st.as_dict() == case["stats"]
 
 
+_EXIT = {}
+
+
+def _exit_oracle(key, field, noise):
+    import oracle
+    if key not in _EXIT:
+        _EXIT.clear()
+        _EXIT[key] = oracle.Oracle(field, noise, exit=True)
+    return _EXIT[key]
+
+
+@pytest.mark.parametrize("case", META, ids=[c["name"] for c in META])
+def test_oracle_exit_tables_keep_golden(built, case):
+    """The build's sun exit tables change no pixel: the oracle
+    marching with them reproduces every golden frame, with no more shadow
+    fetches than the reference's literal march and every other counter equal."""
+    mg = _load()
+    field, noise, fr, w, h = mg.inputs(case)
+    img, st = _exit_oracle(case.get("scene") or case["name"], field, noise).render(fr.params, w, h)
+    _check(mg, case, img)
+    d = st.as_dict()
+    for k, v in case["stats"].items():
+        if k == "shadow_fetches":
+            assert d[k] <= v
+        else:
+            assert d[k] == v, k
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", META, ids=[c["name"] for c in META])
 def test_hip_reproduces_golden(built, case):
@@ -62,7 +90,13 @@ def test_hip_reproduces_golden(built, case):
                   noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
         dev = sc.read_field()
         assert np.array_equal(dev[..., :3], field[..., :3])
-        img, st = sc.render(fr, stats=True)
+        img, st = sc.render(fr, stats=True)                  # with the sun exit tables
+        fr.params.flags |= vx.FLAG_NO_EXIT
+        img_lit, st_lit = sc.render(fr, stats=True)          # every step of the reference's march
     _check(mg, case, img)
+    _check(mg, case, img_lit)
     for k, v in case["stats"].items():
+        assert getattr(st_lit, k) == v, k
+    _, ost = _exit_oracle(case.get("scene") or case["name"], field, noise).render(fr.params, w, h)
+    for k, v in ost.as_dict().items():
         assert getattr(st, k) == v, k

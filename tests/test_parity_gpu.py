@@ -81,7 +81,7 @@ def test_small_frames_bit_exact(seed, dims, sbj, rot, noise):
     with _scene(vx, field, noise, dims) as sc:
         dev_field = sc.read_field()
         img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, 160, 96)
+    ref, ost = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, 160, 96)
     _compare(img, ref)
     g, o = st.as_dict(), ost.as_dict()
     for k in o:
@@ -145,7 +145,7 @@ def test_baseline_sizes_full_frame(full_scene, noise, cfg, cam):
     c = presets.CONFIGS[cfg]
     fr = presets.camera_frame(cam, c["w"], c["h"])
     img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, c["w"], c["h"], threads=16)
+    ref, ost = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, c["w"], c["h"], threads=16)
     _compare(img, ref)
     _counters_equal(st, ost)
     assert st.primary_cap_hits == 0
@@ -234,7 +234,7 @@ def test_edge_params(noise, case):
     with _scene(vx, field, noise, dims) as sc:
         dev_field = sc.read_field()
         img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, 128, 80)
+    ref, ost = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, 128, 80)
     _compare(img, ref)
     assert st.shadow_fetches == ost.shadow_fetches
 
@@ -248,7 +248,7 @@ def test_campus_scene(noise):
     with _scene(vx, field, noise, (1024, 256, 32)) as sc:
         dev_field = sc.read_field()
         img, _ = sc.render(fr)
-    ref, _ = oracle.Oracle(dev_field, noise).render(fr.params, 480, 270, threads=16)
+    ref, _ = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, 480, 270, threads=16)
     _compare(img, ref)
 
 
@@ -286,7 +286,7 @@ def test_extensions_bit_exact(seed, dims, sbj, rot, noise, case):
     with _scene(vx, field, noise, dims) as sc:
         dev_field = sc.read_field()
         img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, 160, 96)
+    ref, ost = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, 160, 96)
     _compare(img, ref)
     g, o = st.as_dict(), ost.as_dict()
     for k in o:
@@ -310,7 +310,7 @@ def test_soft_shadow_paths_at_ragged_sizes(noise, case, w, h):
     with _scene(vx, field, noise, dims) as sc:
         dev_field = sc.read_field()
         img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, w, h)
+    ref, ost = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, w, h)
     _compare(img, ref)
     _counters_equal(st, ost)
 
@@ -330,7 +330,7 @@ def test_extensions_baseline_full_frame(full_scene, noise, cfg, cam, kw):
     c = presets.CONFIGS[cfg]
     fr = presets.camera_frame(cam, c["w"], c["h"], **kw)
     img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(dev_field, noise).render(fr.params, c["w"], c["h"], threads=16)
+    ref, ost = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, c["w"], c["h"], threads=16)
     _compare(img, ref)
     _counters_equal(st, ost)
     assert st.primary_cap_hits == 0
@@ -414,7 +414,7 @@ def test_c5_full_frame_soft_shadows_full_quality(noise):
     own = oracle.field_box(field, main, 32, r_cube=r)
     assert np.array_equal(own, oct_e[main])          # the device's boxes of that octant, at the C5 size
     oct_e[main] = own
-    ref, ost = oracle.Oracle(field, noise, oct_e=oct_e).render(fr.params, c["w"], c["h"], threads=16)
+    ref, ost = oracle.Oracle(field, noise, oct_e=oct_e, exit=True).render(fr.params, c["w"], c["h"], threads=16)
     _compare(img, ref)
     _counters_equal(st, ost)
     assert st.primary_cap_hits == 0
@@ -474,7 +474,7 @@ def test_air_b22_and_b0_render_identically(noise, tmp_path):
         sts.append(st.as_dict() | {"kernel_ms": 0})
     assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
     assert sts[0] == sts[1] and sts[0]["glass_px"] > 100
-    ref, _ = oracle.Oracle(f22, noise).render(fr.params, 160, 96)
+    ref, _ = oracle.Oracle(f22, noise, exit=True).render(fr.params, 160, 96)
     _compare(imgs[0], ref)
 
 
@@ -493,7 +493,7 @@ def test_hand_edited_map_with_large_radii_uses_the_checked_march(noise):
     fr = vx.make_frame((48.0, 24.0, 18.0), (1.1, 0.0, 0.6), 128, 80)
     with _scene(vx, field, noise, dims) as sc:
         img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(field, noise).render(fr.params, 128, 80)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 128, 80)
     _compare(img, ref)
     assert st.shadow_fetches == ost.shadow_fetches
 
@@ -564,7 +564,7 @@ def test_c1_primary_only_every_pixel(noise):
     fr = presets.camera_frame(c["camera"], c["w"], c["h"], flags=vx.FLAG_PRIMARY_ONLY)
     with _scene(vx, field, noise, (1024, 256, 32)) as sc:
         img, st = sc.render(fr, stats=True)
-    ref, ost = oracle.Oracle(field, noise).render(fr.params, c["w"], c["h"])
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, c["w"], c["h"])
     _compare(img, ref)
     for k in ("pixels", "sky_px", "block_px", "glass_px", "primary_fetches"):
         assert getattr(st, k) == getattr(ost, k), k
@@ -590,7 +590,7 @@ def test_c4_full_frame_as_eight_rank_band_lists(full_scene, noise):
     torch.cuda.synchronize()
     img = frame.cpu().numpy()
     del frame
-    ref, _ = oracle.Oracle(dev_field, noise).render(fr.params, w, h, threads=16)
+    ref, _ = oracle.Oracle(dev_field, noise, exit=True).render(fr.params, w, h, threads=16)
     _compare(img, ref)
     del img, ref
     whole = torch.empty((h, w, 4), dtype=torch.uint8, device="cuda:0")
@@ -623,7 +623,7 @@ def test_2d_mode_bit_exact(noise, case):
     with _scene(vx, field, noise, dims) as sc:
         img, st = sc.render(fr, stats=True)
         assert sc.vertex2d() == vx.vertex2d(field)          # the scene's 2D mesh = the host restatement
-    ref, ost = oracle.Oracle(field, noise).render(fr.params, fr.width, fr.height)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, fr.width, fr.height)
     _compare(img, ref)
     for k in ("pixels", "sky_px", "block_px", "glass_px", "primary_fetches"):
         assert getattr(st, k) == getattr(ost, k), k

@@ -29,8 +29,10 @@ FLAG_FULL_QUALITY = FLAG_REFLECT | FLAG_ROUGH
 FLAG_INT_INDEX = 0x40                           # diagnostics: integer primary index path
 FLAG_SOFT_POOL = 0x80                           # soft shadows by the pooled wave march (same frames)
 FLAG_SOFT_BRICK = 0x100                         # + LDS 8^3 brick staging (same frames)
+FLAG_NO_EXIT = 0x200                            # diagnostics: march without the sun exit tables (same frames)
+FLAG_NO_CONE = 0x400                            # diagnostics: orthant exit tables only (same frames)
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 6
+ABI_VERSION = 7
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128
 
@@ -82,6 +84,11 @@ class Stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class ExitInfo(C.Structure):
+    """vx_exit_info (ABI 7): which sun exit copy a frame's march reads."""
+    _fields_ = [("kind", C.c_int), ("octant", C.c_int), ("kx", C.c_int), ("ky", C.c_int)]
+
+
 # (name, restype, argtypes) of every symbol include/voxmap.h declares
 SIGNATURES = [
     ("vx_scene_create", C.c_int, [C.POINTER(SceneDesc), C.POINTER(C.c_void_p)]),
@@ -101,6 +108,7 @@ SIGNATURES = [
     ("vx_render_bands", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
                                   C.POINTER(C.c_int), C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
                                   C.POINTER(Stats)]),
+    ("vx_prepare_sun", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_void_p, C.POINTER(ExitInfo)]),
     ("vx_mgpu_unique_id", C.c_int, [C.c_void_p]),
     ("vx_mgpu_create", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("vx_mgpu_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int, C.c_int,

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -28,6 +29,18 @@ struct vx_scene {
     uint32_t *d_prim = nullptr;   // 8 padded octant copies (vx_internal.h FieldLayout)
     uint8_t *d_sun = nullptr;     // R, G channels
     int8_t *d_sunp = nullptr;     // R, G channels, int8, -1 border (Z <= 126)
+    int8_t *d_sunx = nullptr;     // 8 orthant-exit copies of the march channel (launch_sun_exit)
+    // cone copies of the march channel, built on first use for a frame's sun
+    // samples {octant, kx, ky} (exit_plan) and kept: the sun moves slowly
+    // (map.js:399-402), so one serves many frames
+    struct Cone {
+        int oct = -1, kx = -1, ky = -1;
+        int8_t *d = nullptr;
+        hipEvent_t ready = nullptr;
+        unsigned long long used = 0;
+    } cones[2];
+    unsigned long long cone_tick = 0;
+    std::mutex cone_mu;
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
     uint32_t *d_rg2 = nullptr;    // AO x-pairs: (R, G) of cells x and x + 1, clamped, (X + 1) per row
@@ -176,6 +189,14 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
             if ((e = hipMalloc(&s->d_sunp, 2 * np)) == hipSuccess &&
                 (e = hipMemsetAsync(s->d_sunp, 0xFF, 2 * np, s->stream)) == hipSuccess)
                 lrc = launch_sun_pad(lin, s->d_sunp, X, Y, Z, s->SB, s->stream);
+#ifndef VX_SUNX
+#define VX_SUNX 1
+#endif
+            // per ray octant, the channel with every cell whose orthant ahead holds no block
+            // marked -1: the march exits "lit" there (DESIGN.md §3 "Orthant exit")
+            if (VX_SUNX && !lrc && e == hipSuccess && (e = hipMalloc(&s->d_sunx, 8 * np)) == hipSuccess &&
+                (e = hipMemsetAsync(s->d_sunx, 0xFF, 8 * np, s->stream)) == hipSuccess)
+                lrc = launch_sun_exit(s->d_sunp, s->d_sunx, ga, X, Y, Z, s->SB, s->stream);
             if (e != hipSuccess) lrc = (int)e;
         }
         for (int oct = 0; oct < 8 && !lrc; oct++) {
@@ -203,6 +224,11 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_prim) (void)hipFree(s->d_prim);
     if (s->d_sun) (void)hipFree(s->d_sun);
     if (s->d_sunp) (void)hipFree(s->d_sunp);
+    if (s->d_sunx) (void)hipFree(s->d_sunx);
+    for (auto &c : s->cones) {
+        if (c.d) (void)hipFree(c.d);
+        if (c.ready) (void)hipEventDestroy(c.ready);
+    }
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_rg2) (void)hipFree(s->d_rg2);
     if (s->d_noise4) (void)hipFree(s->d_noise4);
@@ -294,6 +320,62 @@ struct TileSpec {
     int n = 0;
 };
 
+// The frame's cone copy {oct, kx, ky}: found in the scene's cache (the
+// stream waits for its build), or built on stream st into a free or the least
+// recently used slot -- after a device-wide synchronise when that slot's copy
+// may still be read by a frame in flight.
+static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out) {
+    std::lock_guard<std::mutex> lock(s->cone_mu);
+    vx_scene::Cone *slot = nullptr;
+    for (auto &c : s->cones)
+        if (c.d && c.oct == oct && c.kx == kx && c.ky == ky) slot = &c;
+    if (!slot) {
+        slot = &s->cones[0];
+        for (auto &c : s->cones)
+            if (!c.d || c.used < slot->used) slot = &c;
+        if (slot->d) {
+            VX_HIP(hipDeviceSynchronize());
+        } else {
+            const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
+            VX_HIP(hipMalloc(&slot->d, np));
+            if (!slot->ready) VX_HIP(hipEventCreateWithFlags(&slot->ready, hipEventDisableTiming));
+        }
+        slot->oct = -1;
+        VX_HIP(hipMemsetAsync(slot->d, 0xFF, (size_t)s->SXp * s->SYp * s->SZp, st));
+        const int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
+        if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
+        VX_HIP(hipEventRecord(slot->ready, st));
+        slot->oct = oct; slot->kx = kx; slot->ky = ky;
+    } else {
+        VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));
+    }
+    slot->used = ++s->cone_tick;
+    *out = slot->d;
+    return VX_OK;
+}
+
+// The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
+// a.sunc (cone) built or found, and the info filled
+static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &fc, hipStream_t st,
+                      const int8_t **sunc, vx_exit_info *info) {
+    *sunc = nullptr;
+    vx_exit_info e{0, -1, -1, -1};
+    const bool tables = s->d_sunx && !(p->flags & VX_FLAG_NO_EXIT);
+    if (tables && p->quality != 0 && !(p->flags & (VX_FLAG_NO_SHADOW | VX_FLAG_PRIMARY_ONLY))) {
+        int oct, kx, ky;
+        if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
+            const int rc = cone_copy(s, oct, kx, ky, st, sunc);
+            if (rc) return rc;
+            e = vx_exit_info{2, oct, kx, ky};
+        } else if (fc.sun_k[0].fast) {
+            const float *r = fc.sun_k[0].r;
+            e = vx_exit_info{1, (r[0] > 0.0f ? 1 : 0) | (r[1] > 0.0f ? 2 : 0) | (r[2] > 0.0f ? 4 : 0), -1, -1};
+        }
+    }
+    if (info) *info = e;
+    return VX_OK;
+}
+
 static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const TileSpec &ts, int fmt, void *out_dev,
                      void *stream, vx_stats *stats) {
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
@@ -302,6 +384,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.prim = s->d_prim;
     a.sun = s->d_sun;
     a.sunp = s->d_sunp;
+    a.sunx = (p->flags & VX_FLAG_NO_EXIT) ? nullptr : s->d_sunx;
     a.SB = s->SB;
     a.SXp = s->SXp;
     a.SXpYp = (unsigned)s->SXp * (unsigned)s->SYp;
@@ -329,6 +412,10 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.p = *p;
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
+    {
+        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr);
+        if (rc) return rc;
+    }
     a.Xp = s->L.Xp;
     a.pad = s->L.pad;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
@@ -371,6 +458,19 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
         fill_stats(stats, v, ms, fmt == VX_PIXEL_RGBA32F ? 16 : 4);
     }
     return VX_OK;
+}
+
+int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_info *info) {
+    if (!s || !p) return set_error(VX_EINVAL, "vx_prepare_sun: null argument");
+    int rc = check_frame(p, 64, 64, VX_PIXEL_RGBA8);
+    if (rc) return rc;
+    VX_HIP(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    FrameConsts fc;
+    const int max_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;
+    frame_consts(*p, 64, 64, s->X, s->Y, s->Z, max_steps, fc);
+    const int8_t *sunc = nullptr;
+    return frame_exit(s, p, fc, st, &sunc, info);
 }
 
 int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void *out, int out_on_device,

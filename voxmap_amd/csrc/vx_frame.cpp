@@ -148,3 +148,30 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
 }
 
 }  // namespace vx
+
+namespace vx {
+// vx_internal.h exit_plan; the oracle's vxo_exit_plan restated (same double
+// arithmetic on the same fp32 directions, so both pick the same table)
+int exit_plan(const FrameConsts &fc, int SB, int *oct, int *kx, int *ky) {
+    *oct = *kx = *ky = -1;
+    if (fc.n_sun < 1) return 0;
+    const float lim = 0.0009765625f;
+    double ax = 0.0, ay = 0.0;
+    int sg0 = -1;
+    for (int k = 0; k < fc.n_sun; k++) {
+        const float *r = fc.sun_k[k].r;
+        if (!(std::fabs(r[0]) >= lim && std::fabs(r[1]) >= lim && std::fabs(r[2]) >= lim)) return 0;
+        const int sg = (r[0] > 0.0f ? 1 : 0) | (r[1] > 0.0f ? 2 : 0) | (r[2] > 0.0f ? 4 : 0);
+        if (k && sg != sg0) return 0;
+        sg0 = sg;
+        const double sx = std::fabs((double)r[0] / (double)r[2]), sy = std::fabs((double)r[1] / (double)r[2]);
+        ax = sx > ax ? sx : ax;
+        ay = sy > ay ? sy : ay;
+    }
+    // SB = Z + 2 >= 5 >= kx, ky (the window stays inside the -1 border) unless Z < 3
+    if (!(sg0 & 4) || ax > 4.0 || ay > 4.0 || SB < 5) return 0;
+    const int cx = (int)std::ceil(ax + 1.0 / 64.0), cy = (int)std::ceil(ay + 1.0 / 64.0);
+    *oct = sg0; *kx = cx; *ky = cy;
+    return 1;
+}
+}  // namespace vx

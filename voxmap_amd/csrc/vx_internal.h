@@ -72,6 +72,8 @@ struct KernelArgs {
     int SB;                  // border width of sunp (Z + 2: a march step moves <= Z + 1 cells per axis)
     int SXp;                 // padded row length of sunp
     unsigned SXpYp, sunp_texels;
+    const int8_t *sunx;      // 8 orthant-exit copies of sunp's channel, one per ray octant (bit i: r_i > 0), or nullptr
+    const int8_t *sunc;      // the frame's cone-exit copy (every sample of the frame reads it), or nullptr
     const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *rg2;     // AO x-pairs (X + 1 per row): entry p = (R, G) of cells clamp(p - 1), clamp(p)
     const uint32_t *noise;   // RGBA8 noise texels
@@ -142,6 +144,20 @@ int scene_inputs(const vx_scene_desc *d, SceneInputs &in);
 int check_frame(const vx_frame_params *p, int w, int h, int fmt);
 // padded int8 sun channels (border = -1) from the linear RGBA upload
 int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int SB, void *stream);
+// Sun exit tables (DESIGN.md §3 "Sun exit tables"): copies of sunp's march
+// channel with every cell from which the march cannot end unlit set to -1.
+// The 8 orthant copies (sunx, 8 * padded texels; flags = X*Y*Z bytes of
+// scratch), built with the scene, hold for any direction of their octant:
+int launch_sun_exit(const int8_t *sunp, int8_t *sunx, uint8_t *flags, int X, int Y, int Z, int SB, void *stream);
+// a cone copy (one padded channel, border pre-filled with -1) holds for every
+// up-going direction of octant oct whose slopes |r_x/r_z| <= kx - 1/64,
+// |r_y/r_z| <= ky - 1/64 (layer recursion, kx, ky <= SB):
+int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, int oct, int kx, int ky,
+                    void *stream);
+// which copy a frame's sun march reads: 1 = one cone copy {oct, kx, ky} for every
+// sample (all on the fast path, one sign pattern, r_z > 0, slopes <= 4, kx, ky
+// <= SB); 0 = each fast sample its octant's orthant copy (oracle vxo_exit_plan)
+int exit_plan(const FrameConsts &fc, int SB, int *oct, int *kx, int *ky);
 // AO x-pair array from rg: (X + 1) * Y * Z u32 (R, G of two x-neighbours, clamped)
 int launch_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z, void *stream);
 // noise quad texture from the RGBA8 noise: 4 planes (A, R, G, B) of each texel's wrapped 2x2 block

@@ -533,9 +533,11 @@ __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay 
 __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
                                           float f1, float f2, Counters &cnt) {
     if (S.fast && a.sunp) {
-        const int8_t *ch = S.up ? a.sunp : a.sunp + a.sunp_texels;
         // wave-uniform switch on the frame's sun signs: one specialised loop each
         const int sg = (S.sign[0] > 0.0f ? 1 : 0) | (S.sign[1] > 0.0f ? 2 : 0) | (S.sign[2] > 0.0f ? 4 : 0);
+        // the frame's cone copy, else the octant's orthant copy, else the plain channel
+        const int8_t *ch = a.sunc ? a.sunc
+                         : a.sunx ? a.sunx + (size_t)sg * a.sunp_texels : S.up ? a.sunp : a.sunp + a.sunp_texels;
         switch (sg) {
 #define VX_SG(K) case K: return march_pad<K>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
             VX_SG(0) VX_SG(1) VX_SG(2) VX_SG(3) VX_SG(4) VX_SG(5) VX_SG(6)
@@ -1331,7 +1333,9 @@ void k_render(KernelArgs a) {
                 S.r[0] = q0.x; S.r[1] = q0.y; S.r[2] = q0.z;
                 S.abs[0] = q1.x; S.abs[1] = q1.y; S.abs[2] = q1.z;
                 S.rcp[0] = q2.x; S.rcp[1] = q2.y; S.rcp[2] = q2.z;
-                const int8_t *ch = F.sun_k[0].up ? a.sunp : a.sunp + a.sunp_texels;
+                const int8_t *ch = a.sunc ? a.sunc
+                                         : a.sunx ? a.sunx + (size_t)F.soft_sg * a.sunp_texels
+                                         : F.sun_k[0].up ? a.sunp : a.sunp + a.sunp_texels;
                 // EXT 4 is launched only when the bricks fit (launch_render): <= 4 fragments per
                 // pass, 4-byte aligned rows, a border of >= 9 cells around the grid
                 const int sgv = F.soft_sg;
@@ -1775,6 +1779,70 @@ __global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z
     sunp[j] = (int8_t)(t & 0xffu);
     sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);
 }
+// ---- orthant-exit march copies (DESIGN.md §3 "Orthant exit").  For ray
+// octant o (bit i: r_i > 0) and its channel (R if r_z > 0, else G), a cell
+// whose orthant ahead -- every cell c' with c'_i >= c_i on a positive axis,
+// <= on a negative one, inside the grid -- holds no 0 texel becomes -1 (the
+// "left the grid" mark).  Three one-sided OR scans of "texel == 0": along x
+// (one lane per row), y, then z, the last one writing the copy.
+__global__ void k_ox_x(const int8_t *ch, uint8_t *fl, int X, int Y, int Z, int SB, int SXp, size_t SXpYp, int sx) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;     // (y, z) row
+    if (i >= (size_t)Y * Z) return;
+    const int y = (int)(i % Y), z = (int)(i / Y);
+    const int8_t *src = ch + (size_t)SB + (size_t)SXp * (size_t)(y + SB) + SXpYp * (size_t)(z + SB);
+    uint8_t *dst = fl + (size_t)X * i;
+    uint8_t acc = 0;
+    for (int k = 0; k < X; k++) {
+        const int x = sx > 0 ? X - 1 - k : k;                          // from the far end of the ray's side
+        acc |= src[x] == 0 ? 1 : 0;
+        dst[x] = acc;
+    }
+}
+__global__ void k_ox_y(uint8_t *fl, int X, int Y, int Z, int sy) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;     // (x, z), x fastest: coalesced
+    if (i >= (size_t)X * Z) return;
+    const int x = (int)(i % X), z = (int)(i / X);
+    uint8_t *col = fl + (size_t)x + (size_t)X * Y * z;
+    uint8_t acc = 0;
+    for (int k = 0; k < Y; k++) {
+        const int y = sy > 0 ? Y - 1 - k : k;
+        acc |= col[(size_t)X * y];
+        col[(size_t)X * y] = acc;
+    }
+}
+__global__ void k_ox_z(const int8_t *ch, const uint8_t *fl, int8_t *out, int X, int Y, int Z, int SB, int SXp,
+                       size_t SXpYp, int sz) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;     // (x, y), x fastest
+    if (i >= (size_t)X * Y) return;
+    const int x = (int)(i % X), y = (int)(i / X);
+    const size_t p0 = (size_t)(x + SB) + (size_t)SXp * (size_t)(y + SB) + SXpYp * (size_t)SB;
+    uint8_t acc = 0;
+    for (int k = 0; k < Z; k++) {
+        const int z = sz > 0 ? Z - 1 - k : k;
+        acc |= fl[i + (size_t)X * Y * z];
+        const size_t p = p0 + SXpYp * (size_t)z;
+        out[p] = acc ? ch[p] : (int8_t)-1;
+    }
+}
+// One layer z of a cone copy (oracle vxo_field_exit with a finite window):
+// D(x, y, z) = AND over i <= kx, j <= ky of [T(x', y', z) != 0 and
+// D(x', y', z + 1)], x' = x + i*sx, y' = y + j*sy; the channel's and the
+// copy's -1 border make cells outside the grid true (kx, ky <= SB), and layer
+// Z of the copy is border.  Layers are launched from the top down.
+__global__ void k_sun_cone_layer(const int8_t *ch, int8_t *out, int X, int Y, int z, int SB, int SXp, size_t SXpYp,
+                                 int sx, int sy, int kx, int ky) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;     // (x, y), x fastest
+    if (i >= (size_t)X * Y) return;
+    const int x = (int)(i % X), y = (int)(i / X);
+    const size_t p = (size_t)(x + SB) + (size_t)SXp * (size_t)(y + SB) + SXpYp * (size_t)(z + SB);
+    bool d = true;
+    for (int j = 0; j <= ky; j++)
+        for (int k = 0; k <= kx; k++) {
+            const size_t q = p + (ptrdiff_t)(k * sx) + (ptrdiff_t)(j * sy) * SXp;
+            d = d && ch[q] != 0 && out[q + SXpYp] == (int8_t)-1;
+        }
+    out[p] = d ? (int8_t)-1 : ch[p];
+}
 // map.bin B -> the traversal's vis colour, in place in the linear upload (B
 // kept in bcol for vx_scene_read_field): the meshed palette indices 1..21
 // (sdf.cpp:284 meshes colours < pal_size = 22; render.vert:21) stay, anything
@@ -1867,6 +1935,36 @@ int launch_sun_pad(const uint32_t *lin, int8_t *sunp, int X, int Y, int Z, int S
     const size_t N = (size_t)X * Y * Z;
     hipLaunchKernelGGL(k_sun_pad, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lin, sunp, X, Y,
                        Z, SB);
+    return (int)hipGetLastError();
+}
+
+int launch_sun_exit(const int8_t *sunp, int8_t *sunx, uint8_t *flags, int X, int Y, int Z, int SB, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int SXp = X + 2 * SB, SYp = Y + 2 * SB, SZp = Z + 2 * SB;
+    const size_t SXpYp = (size_t)SXp * SYp, np = SXpYp * SZp;
+    const size_t nx = (size_t)Y * Z, ny = (size_t)X * Z, nz = (size_t)X * Y;
+    for (int o = 0; o < 8; o++) {
+        const int sx = o & 1 ? 1 : -1, sy = o & 2 ? 1 : -1, sz = o & 4 ? 1 : -1;
+        const int8_t *ch = sz > 0 ? sunp : sunp + np;          // R for up-going rays, G otherwise
+        hipLaunchKernelGGL(k_ox_x, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s, ch, flags, X, Y, Z, SB, SXp,
+                           SXpYp, sx);
+        hipLaunchKernelGGL(k_ox_y, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0, s, flags, X, Y, Z, sy);
+        hipLaunchKernelGGL(k_ox_z, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, s, ch, flags, sunx + o * np, X,
+                           Y, Z, SB, SXp, SXpYp, sz);
+    }
+    return (int)hipGetLastError();
+}
+
+int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, int oct, int kx, int ky,
+                    void *stream) {
+    if (!(oct & 4) || kx < 0 || ky < 0 || kx > SB || ky > SB) return (int)hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    const int SXp = X + 2 * SB, SYp = Y + 2 * SB;
+    const size_t SXpYp = (size_t)SXp * SYp, n = (size_t)X * Y;
+    const int sx = oct & 1 ? 1 : -1, sy = oct & 2 ? 1 : -1;
+    for (int z = Z - 1; z >= 0; z--)          // R channel (up-going rays), top layer first
+        hipLaunchKernelGGL(k_sun_cone_layer, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sunp, sunc, X, Y, z,
+                           SB, SXp, SXpYp, sx, sy, kx, ky);
     return (int)hipGetLastError();
 }
 

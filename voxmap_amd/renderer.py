@@ -206,6 +206,14 @@ class Scene:
                                     C.byref(st) if st is not None else None))
         return st
 
+    def prepare_sun(self, frame: Frame, *, stream=None) -> dict:
+        """Build (or find) the sun exit copy frame's march reads (vx_prepare_sun,
+        stream-ordered): {"kind": 0 none / 1 orthant / 2 cone, "octant", "kx", "ky"}."""
+        info = _abi.ExitInfo()
+        check(lib().vx_prepare_sun(self.handle, C.byref(frame.params), C.c_void_p(stream) if stream else None,
+                                   C.byref(info)))
+        return {k: getattr(info, k) for k, _ in info._fields_}
+
     def render_bands(self, frame: Frame, band_rows: int, band_ids, out_ptr: int, *, inplace: bool = True,
                      pixel_format=_abi.PIXEL_RGBA8, stream=None, stats: bool = False):
         """Full-width bands of rows (vx_render_bands): in place in a w*h frame, or compact."""
