@@ -183,8 +183,32 @@ def pmc_entry(name, config, cam, flags, samples):
     return None
 
 
+def exit_tables(torch, vx, scene, frame, W, H):
+    """The sun exit copy this frame's march reads (DESIGN.md §3 "Sun exit
+    tables"): which one, the time to build it (vx_prepare_sun on a scene that
+    has not built it yet: a cone copy is built once per sun octant and window,
+    and the sun moves ~1 rad per hour, map.js:399), and the shadow fetches of
+    the same frame without tables -- the reference's own step count."""
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    info = scene.prepare_sun(frame, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    info["build_ms"] = round(1000.0 * (time.perf_counter() - t0), 3)
+    fl = vx.Frame(frame.params.copy(), W, H)
+    fl.params.flags |= vx.FLAG_NO_EXIT
+    out = torch.empty(H * W * 4, dtype=torch.uint8, device="cuda")
+    s0 = scene.render_device(fl, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=st.cuda_stream,
+                             stats=True).as_dict()
+    info["reference_shadow_fetches"] = int(s0["shadow_fetches"])
+    info["reference_alg_bytes"] = int(s0["alg_bytes"])
+    info["kinds"] = "0 none, 1 orthant copies (any sun of the octant), 2 cone copy {octant, kx, ky}"
+    return info
+
+
 def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms):
     """N = 1: K frames in flight over K streams/framebuffers; timings + stats."""
+    ex = exit_tables(torch, vx, scene, frame, W, H)
     streams = [torch.cuda.Stream() for _ in range(K)]
     torch.cuda.set_stream(streams[0])
     outs = [torch.empty(H * W * 4, dtype=torch.uint8, device="cuda") for _ in range(K)]
@@ -199,7 +223,7 @@ def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms):
         n[0] += 1
     wall, settle = timed(torch.cuda.synchronize, step, steps, warmup, settle_ms)
     ev = event_ms(torch, fns[0], steps)
-    return {"wall_s": wall, "settle": settle, "ev_ms": ev, "stats": st.as_dict()}
+    return {"wall_s": wall, "settle": settle, "ev_ms": ev, "stats": st.as_dict(), "exit": ex}
 
 
 def fps_with_d2h(torch, vx, scene, frame, W, H, frames, K=2):
@@ -462,9 +486,11 @@ def main(argv=None):
         del grid
 
     shards = None
+    exit_info = None
     if world == 1:
         r = single_gpu(torch, vx, scene, frame, W, H, K, args.steps, args.warmup, args.settle_ms)
         stats, wall, settle_steps, ev_ms = r["stats"], r["wall_s"], r["settle"], r["ev_ms"]
+        exit_info = r["exit"]
     else:
         stats, wall, settle_steps, shards = multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world,
                                                        local, standin)
@@ -483,7 +509,7 @@ def main(argv=None):
         v1 = {"ms_per_frame": round(ms1w, 4), "mrays_per_s": round(r1 / ms1w / 1e3, 3), "rays_per_frame": int(r1),
               "single_stream_ms_per_frame": round(a["ev_ms"], 4), "alg_bytes": int(s1["alg_bytes"]),
               "roofline_frac": round(roofline_of(s1["alg_bytes"], a["ev_ms"])[1], 4),
-              "lane_util": lane_utils(s1)}
+              "lane_util": lane_utils(s1), "exit_tables": a["exit"]}
     if world == 1 and not args.no_d2h:
         d2h = fps_with_d2h(torch, vx, scene, frame, W, H, max(20, args.steps // 2))
     if world == 1 and cfg_name == "C3" and not args.no_c5 and args.flags is None and args.samples is None:
@@ -511,7 +537,9 @@ def main(argv=None):
               "rays_per_frame": int(rays5), "single_stream_ms_per_frame": round(b["ev_ms"], 4),
               "alg_bytes": int(s5["alg_bytes"]), "roofline_achieved_gbps": round(ach5, 2),
               "roofline_frac": round(frac5, 4), "traffic": t5j.get("hbm_bytes_per_launch") if t5j else None,
-              "lane_util": lane_utils(s5), "scene_build_s": round(t5, 3), "frames": n5}
+              "lane_util": lane_utils(s5), "scene_build_s": round(t5, 3), "frames": n5,
+              "exit_tables": b["exit"],
+              "reference_alg_frac": round(roofline_of(b["exit"]["reference_alg_bytes"], b["ev_ms"])[1], 4)}
         sc5.close()
 
     rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
@@ -573,6 +601,7 @@ def main(argv=None):
                 "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
                 "shadow_rays": int(stats["shadow_rays"]), "reflect_rays": int(stats["reflect_rays"]),
                 "lane_util": lane_utils(stats) if world == 1 else None,
+                "exit_tables": exit_info,
                 "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / wall / 1e6, 3),
                 "v1": v1,
                 "c5": c5,
@@ -592,6 +621,12 @@ def main(argv=None):
                 "frac": round(frac, 4),
                 "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
                 "alg_bytes_per_launch": int(per_launch_bytes),
+                # the same formula over the reference's own step count (every march
+                # step of render.frag:92-136, VX_FLAG_NO_EXIT): what the launch
+                # computes, in the reference algorithm's bytes
+                "reference_alg_bytes_per_launch": exit_info["reference_alg_bytes"] if exit_info else None,
+                "reference_alg_frac": (round(roofline_of(exit_info["reference_alg_bytes"], kernel_ms)[1], 4)
+                                       if exit_info and kernel_ms else None),
                 "avg_launch_ms": round(kernel_ms, 4) if kernel_ms else None,
                 "fabric_gbps": (round(traffic["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 1)
                                 if traffic else None),

@@ -1408,6 +1408,16 @@ void k_render(KernelArgs a) {
                 n_sky = 1;
                 shade_sky(a, d0, d1, d2, rgba, cnt);
             } else {
+                // what a glass pane blends over is shaded FIRST: only its colour
+                // then stays live across the pane's shading (the record g[1]
+                // itself would be: 9 registers, spilled to scratch at the
+                // 64-VGPR budget).  Shading has no side effects besides the
+                // counters (sums), so the order changes no result.
+                float dst[4];
+                if (g[0].id == 2) {
+                    if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
+                    else shade_sky(a, d0, d1, d2, dst, cnt);
+                }
                 float rd[3];
                 shade_block<XE>(a, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
                 if (g[0].id == 2) {
@@ -1423,9 +1433,6 @@ void k_render(KernelArgs a) {
 #pragma unroll
                         for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
                     }
-                    float dst[4];
-                    if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
-                    else shade_sky(a, d0, d1, d2, dst, cnt);
                     const float al = rgba[3];
 #pragma unroll
                     for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
