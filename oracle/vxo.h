@@ -112,6 +112,11 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float dir[3],
  * order; the build blends the first one: DESIGN.md §5).  out: w*h bytes. */
 void vxo_glass_layers(const vxo_scene *s, const vxo_frame *f, int w, int h, uint8_t *out, int n_threads);
 
+/* Diagnostic: per pixel of a tw x th block, the fetch counts of its sun
+ * marches in shading order (-1 past the last), maxrec ints per pixel. */
+void vxo_march_lengths(const vxo_scene *s, const vxo_frame *f, int w, int h, int px0, int py0, int tw, int th,
+                       int *out, int maxrec);
+
 /* Shade one fragment (render.frag:147-252).  out_rgba[3] = alpha. */
 void vxo_shade(const vxo_scene *s, const vxo_frame *f, const vxo_gbuf *g,
                const float prim_dir[3], float out_rgba[4], vxo_stats *st);

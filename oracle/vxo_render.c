@@ -552,6 +552,14 @@ static void rough_normal(const vxo_scene *s, const vxo_gbuf *g, const float n[3]
     out[0] = m[0] / l; out[1] = m[1] / l; out[2] = m[2] / l;
 }
 
+/* Diagnostic recorder (vxo_march_lengths): the fetch count of every sun march
+ * of the pixel being rendered, in order.  Thread-local; NULL = off. */
+static _Thread_local int *g_rec;
+static _Thread_local int g_rec_n, g_rec_cap;
+static inline void rec_march(int fetches) {
+    if (g_rec && g_rec_n < g_rec_cap) g_rec[g_rec_n++] = fetches;
+}
+
 /* Per-frame state derived once (the kernel's FrameConsts play this role). */
 typedef struct {
     const vxo_scene *s;
@@ -726,12 +734,14 @@ static void shade_frag(const shade_ctx *c, const vxo_gbuf *g, const float ray[3]
             march_ex(s, g->cell, g->fract, sunDir, c->max_steps, &sun, c->ex[0]);   /* :233 */
             shadeFactor = shadeFactor * (sun.step == c->max_steps ? 1.0f : 0.0f);   /* :234 */
             if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
+            rec_march(sun.fetches | (sun.step == c->max_steps ? 1 << 16 : 0));
         } else {                 /* ext soft shadows: lit fraction of the sun samples */
             int lit = 0;
             for (int k = 0; k < c->n_sun; k++) {
                 march_ex(s, g->cell, g->fract, c->sun_dirs[k], c->max_steps, &sun, c->ex[k]);
                 lit += sun.step == c->max_steps ? 1 : 0;
                 if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
+                rec_march(sun.fetches | (sun.step == c->max_steps ? 1 << 16 : 0));
             }
             shadeFactor = shadeFactor * ((float)lit / (float)c->n_sun);
         }
@@ -950,4 +960,25 @@ void vxo_render(const vxo_scene *s, const vxo_frame *f, int w, int h,
     if (st) *st = acc;
     ctx_free(&ctx);
     (void)n_threads;
+}
+
+/* Diagnostic (tools/march_sched.py): per pixel of the tw x th block at (px0,
+ * py0) of a w x h frame, the fetch counts of its sun marches in the order the
+ * shading runs them, bit 16 set when the march ended lit (-1 = none beyond),
+ * up to maxrec each, with the scene's exit mode.  Serial. */
+void vxo_march_lengths(const vxo_scene *s, const vxo_frame *f, int w, int h, int px0, int py0, int tw, int th,
+                       int *out, int maxrec) {
+    shade_ctx ctx;
+    ctx_init(&ctx, s, f);
+    ctx_tables(&ctx);
+    float rgba[4];
+    for (int j = 0; j < th; j++)
+        for (int i = 0; i < tw; i++) {
+            int *o = out + ((size_t)j * tw + i) * maxrec;
+            for (int k = 0; k < maxrec; k++) o[k] = -1;
+            g_rec = o; g_rec_n = 0; g_rec_cap = maxrec;
+            if (px0 + i < w && py0 + j < h) render_pixel(&ctx, w, h, px0 + i, py0 + j, rgba, NULL);
+            g_rec = NULL;
+        }
+    ctx_free(&ctx);
 }

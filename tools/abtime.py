@@ -5,7 +5,7 @@ own scene of the same grid, and renders the same frame into the same device
 framebuffer; rounds alternate between variants so clock/thermal drift hits
 all of them alike.  Reports the median ms per frame per variant and flags.
 
-usage: python tools/abtime.py [--config C3] [--flags 0,48] [--rounds 7] [--frames 20] label=path.so ...
+usage: python tools/abtime.py [--config C3] [--flags 0,48] [--rounds 7] [--frames 20] label=path.so[:cap] ...
 """
 from __future__ import annotations
 
@@ -42,6 +42,10 @@ def main():
     libs = []
     for spec in args.variants:
         label, path = spec.split("=", 1)
+        cap = 0
+        if ":" in path:                 # label=lib.so:CAP -- the scene's dist_cap (traversal box cap)
+            path, cap = path.rsplit(":", 1)
+            cap = int(cap)
         L = C.CDLL(os.path.abspath(path))
         for name, res, argt in _abi.SIGNATURES:
             try:
@@ -55,6 +59,7 @@ def main():
         d.map_size = len(gbytes)
         d.map_format = _abi.FORMAT_GRID
         d.X, d.Y, d.Z = X, Y, Z
+        d.dist_cap = cap
         h = C.c_void_p()
         rc = L.vx_scene_create(C.byref(d), C.byref(h))
         if rc:

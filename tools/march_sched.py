@@ -1,0 +1,111 @@
+"""Wave schedules of the soft-shadow marches (a cost model, CPU only).
+
+The oracle records, per pixel of sampled 8x8 tiles (one wave64 each), the
+fetch count of every sun march its shading runs (vxo_march_lengths, with the
+build's exit tables).  Three schedules of a wave's marches are compared, in
+wave steps:
+  lockstep   the kernel's loop: sample k of every lane together; a wave step
+             per step of the longest lane, plus a fixed setup per sample;
+  refill     a lane starts its next march as soon as its march ends; a refill
+             step costs the whole wave `--setup` steps, and runs when at least
+             `--threshold` lanes wait (or every lane is waiting);
+  ideal      no idle lanes: the total fetches / 64.
+usage: python tools/march_sched.py [--config C3] [--samples 16] [--tiles 200]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def lockstep(L, setup):
+    """L: (64, m) fetch counts (-1 = no march); every lane runs its k-th march together."""
+    cost = 0.0
+    for k in range(L.shape[1]):
+        col = L[:, k]
+        if (col >= 0).any():
+            cost += col.max() + setup
+    return cost
+
+
+def refill(L, setup, threshold):
+    queues = [list(r[r >= 0]) for r in L]
+    cur = [q.pop(0) if q else -1 for q in queues]        # remaining steps of the running march
+    cost = setup if any(c >= 0 for c in cur) else 0.0
+    while True:
+        active = [c for c in cur if c > 0]
+        waiting = [i for i, c in enumerate(cur) if c <= 0 and queues[i]]
+        if not active and not waiting:
+            return cost
+        if waiting and (len(waiting) >= threshold or not active):
+            for i in waiting:
+                cur[i] = queues[i].pop(0)
+            cost += setup
+            continue
+        cost += 1
+        cur = [c - 1 if c > 0 else c for c in cur]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--samples", type=int, default=16)
+    ap.add_argument("--tiles", type=int, default=200)
+    ap.add_argument("--setup", type=float, default=0.7, help="per-march setup, in march steps")
+    args = ap.parse_args()
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets, scenes
+    cfg = presets.CONFIGS[args.config]
+    grid = presets.scene_grid(cfg["scene"])
+    field = vx.field_build(grid)
+    noise = scenes.real_noise()
+    W, H = cfg["w"], cfg["h"]
+    fr = presets.camera_frame(cfg["camera"], W, H, flags=vx.FLAG_FULL_QUALITY, shadow_samples=args.samples,
+                              sun_radius=0.03 if args.samples > 1 else 0.0)
+    o = oracle.Oracle(field, noise, exit=True)
+    L = oracle.lib()
+    L.vxo_march_lengths.argtypes = [C.POINTER(oracle.OScene), C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_int, C.c_int, C.c_void_p, C.c_int]
+    L.vxo_march_lengths.restype = None
+    rng = np.random.default_rng(7)
+    maxrec = 2 * max(args.samples, 1) + 2
+    tot = {"lockstep": 0.0, "ideal": 0.0}
+    for t in (4, 8, 16, 32):
+        tot[f"refill_T{t}"] = 0.0
+    n = 0
+    for _ in range(args.tiles):
+        px0 = int(rng.integers(0, W // 8)) * 8
+        py0 = int(rng.integers(0, H // 8)) * 8
+        buf = np.empty((64, maxrec), np.int32)
+        L.vxo_march_lengths(C.byref(o.sc), C.addressof(fr.params), W, H, px0, py0, 8, 8, buf.ctypes.data, maxrec)
+        if not (buf >= 0).any():
+            continue
+        m = buf >= 0
+        lit = (buf >> 16) & 1
+        buf = np.where(m, buf & 0xFFFF, -1)
+        tot.setdefault("fetch_lit", 0); tot.setdefault("fetch_unlit", 0)
+        tot.setdefault("n_lit", 0); tot.setdefault("n_unlit", 0)
+        tot["fetch_lit"] += int(buf[m & (lit == 1)].sum()); tot["fetch_unlit"] += int(buf[m & (lit == 0)].sum())
+        tot["n_lit"] += int((m & (lit == 1)).sum()); tot["n_unlit"] += int((m & (lit == 0)).sum())
+        n += 1
+        tot["lockstep"] += lockstep(buf, args.setup)
+        tot["ideal"] += buf[buf >= 0].sum() / 64.0
+        for t in (4, 8, 16, 32):
+            tot[f"refill_T{t}"] += refill(buf, args.setup, t)
+    print(f"{args.config} samples={args.samples} tiles with marches={n} setup={args.setup} steps")
+    for k in ("fetch_lit", "fetch_unlit", "n_lit", "n_unlit"):
+        print(f"  {k:12s} {tot.pop(k, 0)}")
+    for k, v in tot.items():
+        print(f"  {k:12s} {v / max(n, 1):9.1f} wave steps per wave  ({v / tot['lockstep']:.3f} of lockstep)")
+
+
+if __name__ == "__main__":
+    main()
