@@ -88,6 +88,11 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
         fc.sun_sign[i] = gsign(p.sun_dir[i]);
         fc.sun_abs[i] = std::fabs(p.sun_dir[i]);
         fc.sun_rcp[i] = fc.sun_abs[i] != 0.0f ? 1.0f / fc.sun_abs[i] : 0.0f;
+        const int dim = i == 0 ? X : (i == 1 ? Y : Z);
+        fc.slab_lo[i] = (float)(0 - p.cam_cell[i]) - p.cam_fract[i];
+        fc.slab_hi[i] = (float)(dim - p.cam_cell[i]) - p.cam_fract[i];
+        fc.cell_lo[i] = (float)(-p.cam_cell[i]);
+        fc.cell_hi[i] = (float)(dim - p.cam_cell[i] - 1);
     }
     fc.fw = (float)w;
     fc.fh = (float)h;

@@ -41,6 +41,10 @@ void sun_samples(const float sun[3], float radius, int n, float out[][3]);
 struct FrameConsts {
     int cam_cell[3];
     float cam_fract[3];
+    // primary traversal setup, per axis (the kernel's former per-lane fp32 ops):
+    // grid slab (float)(0 - cam_cell) - cam_fract, (float)(dim - cam_cell) - cam_fract,
+    // and the camera-relative cell range (float)(-cam_cell), (float)(dim - cam_cell - 1)
+    float slab_lo[3], slab_hi[3], cell_lo[3], cell_hi[3];
     float fwd[3], right[3], up[3];
     float fw, fh, rcp_w, rcp_h;        // (float)w, (float)h and RN(1/w), RN(1/h)
     float sun[3];                      // u_sunDir

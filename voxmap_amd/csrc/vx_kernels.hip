@@ -577,32 +577,50 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
     const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
-    float tlo = 0.0f, thi = kInf;
-    float iv0 = kInf, iv1 = kInf, iv2 = kInf;
-    bool miss = false;
-#define VX_SLAB(D, IV, CC, O, DIM)                                          \
-    {                                                                         \
-        const float lo = (float)(0 - CC) - O, hi = (float)(DIM - CC) - O;     \
-        if (D != 0.0f) {                                                      \
-            IV = 1.0f / D;                                                    \
-            float t0 = lo * IV, t1 = hi * IV;                                 \
-            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }           \
-            tlo = gmax(tlo, t0); thi = gmin(thi, t1);                         \
-        } else miss |= !(lo <= 0.0f && 0.0f < hi);                            \
+    // iv = RN(1/d) (kInf for d = 0): rcp_ranged is exact for |d| in [2^-40,
+    // 2^41) -- every lane of nearly every wave (|d| = O(1)); a wave with a lane
+    // outside it (a zero or tiny component) takes the IEEE division
+    float iv0, iv1, iv2;
+    {
+        const unsigned lo_b = 0x2B800000u, span = 0x54000000u - 0x2B800000u;   // 2^-40, 2^41
+        const bool ok = (__float_as_uint(fabsf(d0)) - lo_b) < span && (__float_as_uint(fabsf(d1)) - lo_b) < span &&
+                        (__float_as_uint(fabsf(d2)) - lo_b) < span;
+        if (__builtin_expect(__ballot(!ok) == 0, 1)) {
+            iv0 = rcp_ranged(d0); iv1 = rcp_ranged(d1); iv2 = rcp_ranged(d2);
+        } else {
+            iv0 = d0 != 0.0f ? 1.0f / d0 : kInf;
+            iv1 = d1 != 0.0f ? 1.0f / d1 : kInf;
+            iv2 = d2 != 0.0f ? 1.0f / d2 : kInf;
+        }
     }
-    VX_SLAB(d0, iv0, cc0, o0, a.X)
-    VX_SLAB(d1, iv1, cc1, o1, a.Y)
-    VX_SLAB(d2, iv2, cc2, o2, a.Z)
+    // grid slabs (bounds per frame: FrameConsts::slab_lo/hi); a zero component
+    // misses unless the camera lies inside that slab
+    float tlo = 0.0f, thi = kInf;
+    bool miss = false;
+#define VX_SLAB(D, IV, I)                                                     \
+    {                                                                         \
+        const float lo = F.slab_lo[I], hi = F.slab_hi[I];                     \
+        const float t0 = lo * IV, t1 = hi * IV;                               \
+        const bool sw = t0 > t1, nz = D != 0.0f;                              \
+        tlo = nz ? gmax(tlo, sw ? t1 : t0) : tlo;                             \
+        thi = nz ? gmin(thi, sw ? t0 : t1) : thi;                             \
+        miss |= !nz && !(lo <= 0.0f && 0.0f < hi);                            \
+    }
+    VX_SLAB(d0, iv0, 0)
+    VX_SLAB(d1, iv1, 1)
+    VX_SLAB(d2, iv2, 2)
 #undef VX_SLAB
     if (miss || !(tlo < thi)) return 0;
-    const int c0 = min(max((int)floorf(o0 + tlo * d0), -cc0), a.X - cc0 - 1);
-    const int c1 = min(max((int)floorf(o1 + tlo * d1), -cc1), a.Y - cc1 - 1);
-    const int c2 = min(max((int)floorf(o2 + tlo * d2), -cc2), a.Z - cc2 - 1);
+    // entry cell, camera-relative, as exact fp32 integers: floor, then clamped
+    // into the grid (the former int convert + clamp; o + tlo*d is finite)
+    const float cf0 = __builtin_amdgcn_fmed3f(floorf(o0 + tlo * d0), F.cell_lo[0], F.cell_hi[0]);
+    const float cf1 = __builtin_amdgcn_fmed3f(floorf(o1 + tlo * d1), F.cell_lo[1], F.cell_hi[1]);
+    const float cf2 = __builtin_amdgcn_fmed3f(floorf(o2 + tlo * d2), F.cell_lo[2], F.cell_hi[2]);
     const bool p0 = !(d0 < 0.0f), p1 = !(d1 < 0.0f), p2 = !(d2 < 0.0f);
     const int ip0 = p0, ip1 = p1, ip2 = p2;
     const float s0 = p0 ? 1.0f : -1.0f, s1 = p1 ? 1.0f : -1.0f, s2 = p2 ? 1.0f : -1.0f;
-    const float hp0 = (float)ip0, hp1 = (float)ip1, hp2 = (float)ip2;
-    float h0 = (float)(c0 + ip0), h1 = (float)(c1 + ip1), h2 = (float)(c2 + ip2);
+    const float hp0 = p0 ? 1.0f : 0.0f, hp1 = p1 ? 1.0f : 0.0f, hp2 = p2 ? 1.0f : 0.0f;
+    float h0 = cf0 + hp0, h1 = cf1 + hp1, h2 = cf2 + hp2;
     // padded index of h: kray + hx + Xp*hy + XpYp*hz, mod 2^32 with 24-bit
     // signed products (|h| < 2^23)
     const uint32_t *ppad = a.prim + (size_t)oct * a.copy_texels;
