@@ -212,9 +212,11 @@ int vx_render_tiles(vx_scene *scene, const vx_frame_params *p, int w, int h, int
  * copy frame p will read ahead of time (when the sun moves, off a frame's
  * path) and reports which one it is: kind 0 = none (a sun component below
  * 2^-10, a field without the padded march copy, or VX_FLAG_NO_EXIT), 1 = the
- * orthant copies, 2 = a cone copy. */
+ * orthant copies, 2 = a cone copy.  It synchronises `stream` and, like a call
+ * with stats, uses the scene's timing events (serialise it per scene). */
 typedef struct vx_exit_info {
     int kind, octant, kx, ky;
+    float build_ms;             /* vx_prepare_sun: GPU time of the copy it built (0: already built) */
 } vx_exit_info;
 int vx_prepare_sun(vx_scene *scene, const vx_frame_params *p, void *stream, vx_exit_info *info);
 

@@ -1,0 +1,119 @@
+"""The sun exit tables on the GPU (DESIGN.md §3 "Sun exit tables"): the copy a
+frame reads (vx_prepare_sun) is the one the oracle's restatement of the rule
+picks; frames are bit-identical with the tables, with the orthant copies only
+and with none, over suns that need new cone copies (the scene keeps two, so
+the third evicts one) and frames in flight on two streams right after a sun
+change; the work counters equal the oracle's with the same tables."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(built):
+    if not _gpu():
+        pytest.skip("no GPU visible")
+
+
+@pytest.fixture(scope="module")
+def scene(noise):
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (128, 64, 24)
+    field = vx.field_build(scenes.small_proc(31, dims=dims, n_boxes=20, n_glass=5))
+    sc = vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=dims, device=0)
+    yield sc, field
+    sc.close()
+
+
+def _sun(el_deg, az_deg):
+    el, az = math.radians(el_deg), math.radians(az_deg)
+    return (math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el))
+
+
+# (elevation, azimuth): windows (kx, ky) = (2, 1), (1, 2), (1, 1), (4, 4) in
+# different octants, a low sun (orthant copies) and a sun below the horizon
+SUNS = [(33, 30), (40, 120), (60, 210), (20, 300), (10, 45), (-20, 80)]
+
+
+@pytest.mark.parametrize("el,az", SUNS)
+def test_prepare_sun_matches_the_oracle_rule(scene, el, az):
+    import oracle
+    import voxmap_amd as vx
+    sc, _ = scene
+    sun = _sun(el, az)
+    fr = vx.make_frame((64.0, 32.0, 30.0), (1.0, 0.0, 0.6), 96, 64, sun=sun)
+    info = sc.prepare_sun(fr)
+    cone, octs, kx, ky = oracle.exit_plan([fr.params.sun_dir[:]])
+    if el < 0:
+        assert info["kind"] == 1 or info["kind"] == 0    # below the horizon: shadeFactor is 0 anyway
+    elif cone:
+        assert (info["kind"], info["octant"], info["kx"], info["ky"]) == (2, octs[0], kx, ky)
+    else:
+        assert (info["kind"], info["octant"]) == (1, octs[0])
+    fr.params.flags |= vx.FLAG_NO_EXIT
+    assert sc.prepare_sun(fr)["kind"] == 0
+
+
+def test_frames_identical_across_sun_changes_and_table_modes(scene, noise):
+    """Cycle through suns needing four different copies (two cache slots: every
+    new one evicts), render each with cone, orthant and no tables: identical
+    RGBA32F frames, and counters equal to the oracle's with the same tables."""
+    import oracle
+    import voxmap_amd as vx
+    sc, field = scene
+    o = oracle.Oracle(sc.read_field(), noise, exit=True)
+    for rep in range(2):
+        for el, az in SUNS[:4] + SUNS[:2]:
+            sun = _sun(el, az)
+            fr = vx.make_frame((40.0, 20.0, 26.0), (1.1, 0.0, 0.5 + 0.3 * rep), 128, 72, sun=sun,
+                               flags=vx.FLAG_FULL_QUALITY)
+            img, st = sc.render(fr, stats=True)
+            ref, ost = o.render(fr.params, 128, 72)
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (el, az)
+            assert st.as_dict()["shadow_fetches"] == ost.as_dict()["shadow_fetches"]
+            for fl in (vx.FLAG_NO_CONE, vx.FLAG_NO_EXIT):
+                f2 = vx.make_frame((40.0, 20.0, 26.0), (1.1, 0.0, 0.5 + 0.3 * rep), 128, 72, sun=sun,
+                                   flags=vx.FLAG_FULL_QUALITY | fl)
+                img2 = sc.render(f2)
+                if isinstance(img2, tuple):
+                    img2 = img2[0]
+                assert np.array_equal(img2.view(np.uint32), img.view(np.uint32)), (el, az, fl)
+
+
+def test_two_streams_right_after_a_sun_change(scene):
+    """A new sun's cone copy is built on the first frame's stream; a frame
+    launched at once on a second stream must wait for it (hipStreamWaitEvent):
+    both RGBA8 frames equal the single-stream frame, for several sun changes."""
+    import torch
+
+    import voxmap_amd as vx
+    sc, _ = scene
+    W, H = 256, 160
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.empty(W * H * 4, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    for el, az in [(25, 15), (35, 140), (50, 250), (28, 320), (25, 15)]:
+        fr = vx.make_frame((64.0, 32.0, 34.0), (1.0, 0.0, -0.4), W, H, sun=_sun(el, az),
+                           flags=vx.FLAG_FULL_QUALITY)
+        sc.render_device(fr, a.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=s1.cuda_stream)
+        sc.render_device(fr, b.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+        ref = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
+        if isinstance(ref, tuple):
+            ref = ref[0]
+        ref = np.ascontiguousarray(ref).view(np.uint8).ravel()
+        assert np.array_equal(a.cpu().numpy(), ref), (el, az)
+        assert np.array_equal(b.cpu().numpy(), ref), (el, az)

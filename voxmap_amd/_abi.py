@@ -86,7 +86,7 @@ class Stats(C.Structure):
 
 class ExitInfo(C.Structure):
     """vx_exit_info (ABI 7): which sun exit copy a frame's march reads."""
-    _fields_ = [("kind", C.c_int), ("octant", C.c_int), ("kx", C.c_int), ("ky", C.c_int)]
+    _fields_ = [("kind", C.c_int), ("octant", C.c_int), ("kx", C.c_int), ("ky", C.c_int), ("build_ms", C.c_float)]
 
 
 # (name, restype, argtypes) of every symbol include/voxmap.h declares

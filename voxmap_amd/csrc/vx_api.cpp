@@ -324,7 +324,8 @@ struct TileSpec {
 // stream waits for its build), or built on stream st into a free or the least
 // recently used slot -- after a device-wide synchronise when that slot's copy
 // may still be read by a frame in flight.
-static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out) {
+static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built) {
+    *built = false;
     std::lock_guard<std::mutex> lock(s->cone_mu);
     vx_scene::Cone *slot = nullptr;
     for (auto &c : s->cones)
@@ -346,6 +347,7 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
         VX_HIP(hipEventRecord(slot->ready, st));
         slot->oct = oct; slot->kx = kx; slot->ky = ky;
+        *built = true;
     } else {
         VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));
     }
@@ -357,21 +359,23 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
 // a.sunc (cone) built or found, and the info filled
 static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &fc, hipStream_t st,
-                      const int8_t **sunc, vx_exit_info *info) {
+                      const int8_t **sunc, vx_exit_info *info, bool *built = nullptr) {
     *sunc = nullptr;
-    vx_exit_info e{0, -1, -1, -1};
+    bool b = false;
+    vx_exit_info e{0, -1, -1, -1, 0.0f};
     const bool tables = s->d_sunx && !(p->flags & VX_FLAG_NO_EXIT);
     if (tables && p->quality != 0 && !(p->flags & (VX_FLAG_NO_SHADOW | VX_FLAG_PRIMARY_ONLY))) {
         int oct, kx, ky;
         if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
-            const int rc = cone_copy(s, oct, kx, ky, st, sunc);
+            const int rc = cone_copy(s, oct, kx, ky, st, sunc, &b);
             if (rc) return rc;
-            e = vx_exit_info{2, oct, kx, ky};
+            e = vx_exit_info{2, oct, kx, ky, 0.0f};
         } else if (fc.sun_k[0].fast) {
             const float *r = fc.sun_k[0].r;
-            e = vx_exit_info{1, (r[0] > 0.0f ? 1 : 0) | (r[1] > 0.0f ? 2 : 0) | (r[2] > 0.0f ? 4 : 0), -1, -1};
+            e = vx_exit_info{1, (r[0] > 0.0f ? 1 : 0) | (r[1] > 0.0f ? 2 : 0) | (r[2] > 0.0f ? 4 : 0), -1, -1, 0.0f};
         }
     }
+    if (built) *built = b;
     if (info) *info = e;
     return VX_OK;
 }
@@ -470,7 +474,18 @@ int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_
     const int max_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;
     frame_consts(*p, 64, 64, s->X, s->Y, s->Z, max_steps, fc);
     const int8_t *sunc = nullptr;
-    return frame_exit(s, p, fc, st, &sunc, info);
+    bool built = false;
+    VX_HIP(hipEventRecord(s->ev0, st));
+    rc = frame_exit(s, p, fc, st, &sunc, info, &built);
+    if (rc) return rc;
+    VX_HIP(hipEventRecord(s->ev1, st));
+    VX_HIP(hipStreamSynchronize(st));
+    if (info && built) {
+        float ms = 0.0f;
+        VX_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        info->build_ms = ms;
+    }
+    return VX_OK;
 }
 
 int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void *out, int out_on_device,

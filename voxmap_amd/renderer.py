@@ -208,7 +208,8 @@ class Scene:
 
     def prepare_sun(self, frame: Frame, *, stream=None) -> dict:
         """Build (or find) the sun exit copy frame's march reads (vx_prepare_sun,
-        stream-ordered): {"kind": 0 none / 1 orthant / 2 cone, "octant", "kx", "ky"}."""
+        synchronises the stream): {"kind": 0 none / 1 orthant / 2 cone, "octant",
+        "kx", "ky", "build_ms": GPU time of the copy built now (0: already built)}."""
         info = _abi.ExitInfo()
         check(lib().vx_prepare_sun(self.handle, C.byref(frame.params), C.c_void_p(stream) if stream else None,
                                    C.byref(info)))
