@@ -526,6 +526,34 @@ __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay 
     return step == maxs;
 }
 
+// The first step of a march from a face (DESIGN.md §3 "Sun exit tables", the
+// first step).  A fragment starts on its face plane (f = 0 on the face axis a)
+// with the in-face fracts f_j, f_k; when the sun lies on the face's normal
+// side, the first step -- len <= sqrt(3) * 1e-4/|r_a| (a tie takes the literal
+// length), so it moves under 0.2 cell on the other axes -- lands in the air
+// cell on the normal side or a neighbour of it toward the sun on the in-face
+// axes (f_j, f_k in [0, 1)): the 2 x 2 block of bit a.  If the air cell's value
+// in the exit copy carries bit a, every cell the step can land in is marked,
+// so the march ends there, lit, with no fetch counted: the same lit flag and
+// counters without its setup, first step and load.  Used for the soft-shadow
+// samples of a fragment (one test for all of them); for the single hard
+// shadow it measured +-0 on C3.  ch = the exit copy every sample reads (sg =
+// their sign pattern, fast path); true = lit.
+__device__ __forceinline__ bool first_step_exit(const KernelArgs &a, const int8_t *ch, int sg, const Surf &g) {
+    if (a.fc.max_steps < 1) return false;
+    const int ax = g.nidx >> 1;
+    const bool nneg = (g.nidx & 1) != 0;                   // face normal -e_a (render.vert:14-17)
+    const bool spos = (sg >> ax) & 1;                      // sun toward +e_a
+    const float fj = ax == 0 ? g.f1 : g.f0, fk = ax == 2 ? g.f1 : g.f2;
+    const bool ok = spos != nneg && fj >= 0.0f && fj < 1.0f && fk >= 0.0f && fk < 1.0f;
+    const int x = g.c0 - (ax == 0 && nneg ? 1 : 0), y = g.c1 - (ax == 1 && nneg ? 1 : 0),
+              z = g.c2 - (ax == 2 && nneg ? 1 : 0);
+    // the air cell is inside the padded copy (a face lies inside the grid or on its edge)
+    const unsigned off = (unsigned)(x + a.SB) + (unsigned)a.SXp * (unsigned)(y + a.SB) + a.SXpYp * (unsigned)(z + a.SB);
+    const float v = ok ? ld_fmt1(buf_rsrc(ch, kRsrcS8), off) : 0.0f;
+    return v <= -2.0f && (((int)(-1.0f - v) >> ax) & 1);
+}
+
 // march(cell, fract, S.r) of render.frag:233 -> "lit" (step == MAX_STEPS, :234).
 // S by value: the soft-shadow loop indexes sun_k[k] dynamically, and a
 // reference into the kernel argument there made the compiler copy the whole
@@ -985,12 +1013,22 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
     if (rough)
         shadeFactor = F.sun[2] < 0.0f ? 0.0f : sqrtf(gmax(0.0f, (m0 * F.sun[0] + m1 * F.sun[1]) + m2 * F.sun[2]));
     if (shadeFactor > 0.0f && !(F.flags & VX_FLAG_NO_SHADOW)) {                        // :232-235
+        // the exit copy every sample reads (sunc, or the octant's orthant copy
+        // when they share one sign pattern): a first step into a marked block is lit
+        const int sg0 = (F.sun_k[0].sign[0] > 0.0f ? 1 : 0) | (F.sun_k[0].sign[1] > 0.0f ? 2 : 0) |
+                        (F.sun_k[0].sign[2] > 0.0f ? 4 : 0);
+        const int8_t *xch = EXT != 2 || !a.sunp || !F.sun_k[0].fast ? nullptr
+                          : a.sunc ? a.sunc
+                          : a.sunx && F.soft_sg >= 0 ? a.sunx + (size_t)sg0 * a.sunp_texels : nullptr;
+        const bool first_exit = xch && lit_given < 0 && first_step_exit(a, xch, sg0, g);
         if (EXT != 2) {                // the reference's hard shadow: one sun ray
             cnt.shadow_rays++;
             const bool lit = march_sun(a, F.sun_k[0], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt);
             shadeFactor = shadeFactor * (lit ? 1.0f : 0.0f);
         } else if (lit_given >= 0) {   // marched by the wave pass (k_render)
             shadeFactor = shadeFactor * ((float)lit_given / (float)F.n_sun);
+        } else if (first_exit) {       // every sample's first step lands in the marked block
+            cnt.shadow_rays += (unsigned)F.n_sun;
         } else {                       // ext soft shadows (EXT == 2): lit fraction of the sun samples
             int lit = 0;
             for (int k = 0; k < F.n_sun; k++) {
@@ -1804,6 +1842,26 @@ __global__ void k_sun_pad(const uint32_t *src, int8_t *sunp, int X, int Y, int Z
     sunp[j] = (int8_t)(t & 0xffu);
     sunp[Xp * Yp * Zp + j] = (int8_t)((t >> 8) & 0xffu);
 }
+// ---- first-step bits of an exit copy (DESIGN.md §3 "Sun exit tables", the
+// first step).  A marked cell c (value < 0) gets bit a (a = face axis) when
+// the 2 x 2 block c + {0, s_j} x {0, s_k} of the two other axes is marked
+// too: the value becomes -1 - bits (-1 .. -8; every negative value is the
+// march's exit).  k_render reads the bits at a fragment's air cell: a first
+// step from the face lands in that block, so the march can end before it.
+__global__ void k_exit_face_bits(int8_t *cp, int X, int Y, int Z, int SB, int SXp, size_t SXpYp, int sx, int sy,
+                                 int sz) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)X * Y * Z) return;
+    const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+    const size_t p = (size_t)(x + SB) + (size_t)SXp * (size_t)(y + SB) + SXpYp * (size_t)(z + SB);
+    if (cp[p] >= 0) return;
+    const ptrdiff_t dx = sx, dy = (ptrdiff_t)sy * SXp, dz = (ptrdiff_t)sz * (ptrdiff_t)SXpYp;
+    auto m = [&](ptrdiff_t o) { return cp[p + o] < 0; };      // marked (any negative value, border included)
+    const int bx = m(dy) && m(dz) && m(dy + dz);
+    const int by = m(dx) && m(dz) && m(dx + dz);
+    const int bz = m(dx) && m(dy) && m(dx + dy);
+    cp[p] = (int8_t)(-1 - (bx | (by << 1) | (bz << 2)));
+}
 // ---- orthant-exit march copies (DESIGN.md §3 "Orthant exit").  For ray
 // octant o (bit i: r_i > 0) and its channel (R if r_z > 0, else G), a cell
 // whose orthant ahead -- every cell c' with c'_i >= c_i on a positive axis,
@@ -1976,6 +2034,9 @@ int launch_sun_exit(const int8_t *sunp, int8_t *sunx, uint8_t *flags, int X, int
         hipLaunchKernelGGL(k_ox_y, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0, s, flags, X, Y, Z, sy);
         hipLaunchKernelGGL(k_ox_z, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, s, ch, flags, sunx + o * np, X,
                            Y, Z, SB, SXp, SXpYp, sz);
+        const size_t n = (size_t)X * Y * Z;
+        hipLaunchKernelGGL(k_exit_face_bits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sunx + o * np, X, Y,
+                           Z, SB, SXp, SXpYp, sx, sy, sz);
     }
     return (int)hipGetLastError();
 }
@@ -1990,6 +2051,9 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
     for (int z = Z - 1; z >= 0; z--)          // R channel (up-going rays), top layer first
         hipLaunchKernelGGL(k_sun_cone_layer, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sunp, sunc, X, Y, z,
                            SB, SXp, SXpYp, sx, sy, kx, ky);
+    const size_t nc = n * Z;
+    hipLaunchKernelGGL(k_exit_face_bits, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, sunc, X, Y, Z, SB, SXp,
+                       SXpYp, sx, sy, 1);
     return (int)hipGetLastError();
 }
 
