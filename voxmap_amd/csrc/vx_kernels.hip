@@ -277,6 +277,19 @@ __device__ __forceinline__ float march_len(const SunRay &S, float f0, float f1, 
 // the fast paths have no zero component): fract(-f*s) + 1e-4 without the
 // multiply -- for s > 0 it is (-f) - floor(-f) = ceil(f) - f, the same single
 // IEEE subtraction (floor(-f) = -ceil(f)); for s < 0, f - floor(f).
+// the step length from the distance terms d_i = fract(-f_i*s_i) + 1e-4 (:94-105)
+__device__ __forceinline__ float march_len_d(const SunRay &S, float d0, float d1, float d2) {
+    const float t0 = div_const(d0, S.abs[0], S.rcp[0]);                                // :97
+    const float t1 = div_const(d1, S.abs[1], S.rcp[1]);
+    const float t2 = div_const(d2, S.abs[2], S.rcp[2]);
+    float len = __builtin_fminf(__builtin_fminf(t0, t1), t2);                         // :100-105, one axis
+    if (__builtin_amdgcn_fmed3f(t0, t1, t2) == len) {                                  // ties: literal length
+        const float v0 = t0 == len ? t0 : 0.0f, v1 = t1 == len ? t1 : 0.0f, v2 = t2 == len ? t2 : 0.0f;
+        len = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+    }
+    return len;
+}
+
 template <int SG>
 __device__ __forceinline__ float march_len_sg(const SunRay &S, float f0, float f1, float f2) {
     const float d0 = ((SG & 1) ? ceilf(f0) - f0 : f0 - floorf(f0)) + 1e-4f;
@@ -375,19 +388,18 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
 // biased fp32 integer exy (2^23 <= exy < 2^24) and moved by fma(fl1, Xp, fl0)
 // per step.  The texel arrives as a float (kRsrcS8): safe directly, -1 = left
 // the grid.
-template <int SG>   // the sun's axis signs (bit i: r_i > 0)
-__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
-                                          int c2, float f0, float f1, float f2, Counters &cnt) {
+// march_pad's loop from a start state: exy, e2 = the start cell's biased
+// offset terms, len = the first step's length (march_len_sg), rsrc = the
+// channel's typed-load descriptor (march_pad; march_soft shares these across
+// the samples of a fragment).
+template <int SG>
+__device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay &S, u32x4 rsrc, float exy, float e2,
+                                               float len, float f0, float f1, float f2, Counters &cnt) {
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = a.fc.max_steps;
     if (maxs <= 0) return maxs == 0;
     const float xpf = (float)a.SXp;
-    constexpr float kBias = 8388608.0f;
-    float exy = __builtin_fmaf((float)(c1 + a.SB), xpf, (float)(c0 + a.SB) + kBias);
-    float e2 = (float)(c2 + a.SB) + kBias;
     const unsigned sxpyp = a.SXpYp;
-    const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);   // (pointer arithmetic: keeps the global address space)
-    float len = march_len_sg<SG>(S, f0, f1, f2);
     float tv = 1.0f;                            // texel of the current cell = safe (render.frag:86: 1)
     // one step of :94-128 -> the offset of the texel to load
     auto advance = [&]() -> unsigned {
@@ -425,6 +437,42 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
         cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
     }
     return tv != 0.0f;
+}
+
+template <int SG>   // the sun's axis signs (bit i: r_i > 0)
+__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
+                                          int c2, float f0, float f1, float f2, Counters &cnt) {
+    const float xpf = (float)a.SXp;
+    constexpr float kBias = 8388608.0f;
+    const float exy = __builtin_fmaf((float)(c1 + a.SB), xpf, (float)(c0 + a.SB) + kBias);
+    const float e2 = (float)(c2 + a.SB) + kBias;
+    const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);   // (pointer arithmetic: keeps the global address space)
+    return march_pad_from<SG>(a, S, rsrc, exy, e2, march_len_sg<SG>(S, f0, f1, f2), f0, f1, f2, cnt);
+}
+
+// The soft-shadow samples of one fragment (every sample on the padded path with
+// sign pattern SG, all reading `sun`): the start cell's offset terms, the
+// descriptor and the first step's fract terms d_i are the same for every
+// sample, so they are formed once; only the three quotients by |r_k| differ.
+template <int SG>
+__device__ __forceinline__ int march_soft(const KernelArgs &a, const int8_t *sun, int c0, int c1, int c2, float f0,
+                                          float f1, float f2, Counters &cnt) {
+    const FrameConsts &F = a.fc;
+    const float xpf = (float)a.SXp;
+    constexpr float kBias = 8388608.0f;
+    const float exy = __builtin_fmaf((float)(c1 + a.SB), xpf, (float)(c0 + a.SB) + kBias);
+    const float e2 = (float)(c2 + a.SB) + kBias;
+    const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);
+    const float d0 = ((SG & 1) ? ceilf(f0) - f0 : f0 - floorf(f0)) + 1e-4f;     // march_len_sg's terms
+    const float d1 = ((SG & 2) ? ceilf(f1) - f1 : f1 - floorf(f1)) + 1e-4f;
+    const float d2 = ((SG & 4) ? ceilf(f2) - f2 : f2 - floorf(f2)) + 1e-4f;
+    int lit = 0;
+    for (int k = 0; k < F.n_sun; k++) {
+        cnt.shadow_rays++;
+        const SunRay S = F.sun_k[k];
+        lit += march_pad_from<SG>(a, S, rsrc, exy, e2, march_len_d(S, d0, d1, d2), f0, f1, f2, cnt) ? 1 : 0;
+    }
+    return lit;
 }
 
 // march_pad with an LDS brick (VX_FLAG_SOFT_BRICK, the EXT 4 instantiation:
@@ -1031,9 +1079,18 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
             cnt.shadow_rays += (unsigned)F.n_sun;
         } else {                       // ext soft shadows (EXT == 2): lit fraction of the sun samples
             int lit = 0;
-            for (int k = 0; k < F.n_sun; k++) {
-                cnt.shadow_rays++;
-                lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt) ? 1 : 0;
+            if (xch) {                 // one sign pattern, one copy: the shared-start loop
+                switch (sg0) {
+#define VX_SGS(K) case K: lit = march_soft<K>(a, xch, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt); break;
+                    VX_SGS(0) VX_SGS(1) VX_SGS(2) VX_SGS(3) VX_SGS(4) VX_SGS(5) VX_SGS(6)
+                    default: lit = march_soft<7>(a, xch, g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt);
+#undef VX_SGS
+                }
+            } else {
+                for (int k = 0; k < F.n_sun; k++) {
+                    cnt.shadow_rays++;
+                    lit += march_sun(a, F.sun_k[k], g.c0, g.c1, g.c2, g.f0, g.f1, g.f2, cnt) ? 1 : 0;
+                }
             }
             shadeFactor = shadeFactor * ((float)lit / (float)F.n_sun);
         }
