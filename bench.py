@@ -707,6 +707,26 @@ def cpu_baseline(scene, noise, frame, W, H, target_s):
     _, st1 = o.render(frame.params, W, H, row0=k1 // 2, row_step=k1, threads=1, out=out)
     dt1 = time.perf_counter() - t0
     single = (st1.pixels + st1.shadow_rays + st1.reflect_rays) / dt1 / 1e6
+    # the same frame by the oracle with this build's sun exit tables (the table
+    # built once, outside the timing, as the GPU builds it once per sun window):
+    # what the GPU's algorithm runs at on these cores
+    same = None
+    try:
+        oe = oracle.Oracle(field, noise, exit=True)
+        held = oe.hold_exit_table(frame.params)
+        er = []
+        t_end = time.perf_counter() + target_s / 3
+        while time.perf_counter() < t_end or len(er) < 2:
+            t0 = time.perf_counter()
+            _, se = oe.render(frame.params, W, H, threads=threads, out=out)
+            er.append((se.pixels + se.shadow_rays + se.reflect_rays) / (time.perf_counter() - t0) / 1e6)
+            if len(er) >= 30:
+                break
+        same = {"value": round(float(np.median(er)), 4), "unit": "Mrays/s", "cores": threads,
+                "sample": f"{len(er)} full {W}x{H} frames, median rate, exit table {held} held",
+                "shadow_fetches": int(se.shadow_fetches)}
+    except Exception as e:              # a diagnostic: never lose the baseline over it
+        same = {"error": str(e)}
     return {
         "value": round(float(np.median(rates)), 4),
         "unit": "Mrays/s",
@@ -716,6 +736,7 @@ def cpu_baseline(scene, noise, frame, W, H, target_s):
         "single_core": {"value": round(single, 4), "unit": "Mrays/s", "cores": 1,
                         "sample": f"rows {k1 // 2}::{k1} of the same {W}x{H} frame ({st1.pixels} pixels) "
                                   f"in {dt1:.2f} s"},
+        "same_algorithm": same,
         "host": {"threads_used": threads, "affinity_cores": aff, "hardware_concurrency": node,
                  "note": "the GPU box allots 16 host cores to a 1-GPU job (OMP_NUM_THREADS=16); "
                          "the oracle scales ~linearly over rows (independent pixels)"},

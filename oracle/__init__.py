@@ -23,7 +23,8 @@ LIB_PATH = os.path.join(_HERE, "build", "libvxo.so")
 class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
                 ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p),
-                ("exit_mode", C.c_int)]
+                ("exit_mode", C.c_int), ("held", C.c_void_p), ("held_oct", C.c_int), ("held_kx", C.c_int),
+                ("held_ky", C.c_int)]
 
 
 class OStats(C.Structure):
@@ -121,6 +122,20 @@ class Oracle:
             mode = 2 if exit == "orthant" else 1
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
                          (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data, mode)
+
+    def hold_exit_table(self, params):
+        """Build the exit table the frame `params` reads (exit mode, every sample
+        on one table) once and keep it, so renders of that sun skip the build."""
+        if not self.sc.exit_mode:
+            return None
+        d = sun_samples(params.sun_dir[:], params.sun_radius, params.shadow_samples)
+        cone, octs, kx, ky = exit_plan(d, allow_cone=self.sc.exit_mode == 1 and self.sc.Z >= 3)
+        if len(set(octs)) != 1 or octs[0] < 0:
+            return None
+        self._held = field_exit(self.field, octs[0], kx, ky)
+        self.sc.held = self._held.ctypes.data
+        self.sc.held_oct, self.sc.held_kx, self.sc.held_ky = octs[0], kx, ky
+        return octs[0], kx, ky
 
     def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
         """RGBA fp32 (h, w, 4); rows not in (row0::row_step) are NaN."""

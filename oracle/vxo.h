@@ -43,6 +43,10 @@ typedef struct {
                                  1: the build's sun exit tables (vxo_field_exit, chosen per frame by
                                  vxo_exit_plan), so the shadow fetch counters equal the kernel's; frames are
                                  identical either way.  2: orthant tables only (VX_FLAG_NO_CONE). */
+    const uint8_t *held;      /* a table the caller built (vxo_field_exit) and keeps, for {held_oct, held_kx,
+                                 held_ky}: a frame whose plan needs exactly that table reads it instead of
+                                 building its own (the CPU baseline's timed frames); NULL = none */
+    int held_oct, held_kx, held_ky;
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */

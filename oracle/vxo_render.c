@@ -594,6 +594,10 @@ static void ctx_tables(shade_ctx *c) {
         int found = -1;
         for (int j = 0; j < c->n_owned; j++)
             if (key[j] == oct[k]) found = j;
+        if (found < 0 && s->held && s->held_oct == oct[k] && s->held_kx == kx && s->held_ky == ky) {
+            c->ex[k] = s->held;
+            continue;
+        }
         if (found < 0) {
             uint8_t *t = (uint8_t *)malloc((size_t)s->X * s->Y * s->Z);
             vxo_field_exit(s->field, s->X, s->Y, s->Z, oct[k], kx, ky, t);
