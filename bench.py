@@ -53,10 +53,12 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames alternate over this many streams and framebuffers "
-                         "(double buffering), so one frame's launch gap and tail overlap the next (~6%%, "
-                         "profiles/r01_overlap.txt); 1 = one stream")
+                         "(a swap chain), so one frame's ramp-down overlaps the next frames' blocks. Default 4 on "
+                         "one GPU (one stream per hardware queue: C3 full quality -4.8 %% against 2, "
+                         "profiles/r03_ab_row_stride.txt), 2 at N > 1 (the RCCL gathers share one communicator); "
+                         "1 = one stream")
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed frames rendered before the warmup so the GPU clock leaves its idle state "
                          "(a ~5 ms burst runs ~12%% slower than steady state: profiles/r01_clock_settle.txt)")
@@ -468,7 +470,7 @@ def main(argv=None):
     samples = args.samples if args.samples is not None else cfg.get("samples", 1)
     frame = presets.camera_frame(cam, W, H, scale=up, flags=flags, shadow_samples=samples,
                                  sun_radius=args.sun_radius if samples > 1 else 0.0)
-    K = max(1, args.inflight)
+    K = max(1, args.inflight if args.inflight is not None else (4 if world == 1 else 2))
 
     X = Y = Z = 0
     t_scene = 0.0
