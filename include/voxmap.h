@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 7
+#define VX_ABI_VERSION 8
 
 /* error codes */
 #define VX_OK 0
@@ -95,6 +95,26 @@ extern "C" {
 #define VX_FLAG_NO_EXIT 0x200u
 /* Diagnostics: the orthant exit tables only, no per-sun cone table.  Identical frames. */
 #define VX_FLAG_NO_CONE 0x400u
+/* Diagnostics (ABI 8): the unit-cell G-buffer split of ABI <= 7.  By default a
+ * fragment carries what the raster hands render.frag: v_cellPos = the origin of
+ * the greedy quad that covers its face, v_fractPos = the hit point minus that
+ * origin (render.vert:25-28, quads sdf.cpp:284-356).  With this
+ * flag v_cellPos is the hit cell and v_fractPos the hit's fraction in it: the
+ * same point, another fp32 split. */
+#define VX_FLAG_UNIT_GBUF 0x800u
+/* Glass in draw order (ABI 8): every front-facing glass face in
+ * front of the opaque surface is blended as the reference's raster does --
+ * glass quads after all opaque ones, in vertex.bin order (sdf.cpp:284,337),
+ * depth test LESS with depth writes on, SRC_ALPHA blending (render.js:82-91) --
+ * instead of the single layer (the nearest pane over the surface behind it).
+ * The nearest VX_MAX_GLASS_LAYERS panes of a pixel take part. */
+#define VX_FLAG_GLASS_ORDER 0x1000u
+#define VX_MAX_GLASS_LAYERS 8
+/* Extension (ABI 8): every primary fragment mirrors the traced scene, as
+ * VX_FLAG_REFLECT does for glass: the first surface (and what a pane blends
+ * over) adds Schlick F * the colour along its mirror ray (DESIGN.md §3
+ * "Extensions"; README.md:18-25 describes a reflection pass over the frame). */
+#define VX_FLAG_REFLECT_ALL 0x2000u
 #define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;
@@ -118,6 +138,8 @@ typedef struct vx_scene_desc {
     int device;                 /* HIP device ordinal */
     int dist_cap;               /* air-cube size cap of the primary traversal (and border width), 0 -> 32 */
     uint32_t noise_seed;        /* seed of the synthetic noise when none is given */
+    int mesh_chunk;             /* ABI 8: CHUNK of the greedy mesh whose quads give the G-buffer split
+                                   (voxmap.h:9, sdf.cpp:284-356); 0 -> Z; at most 255 */
 } vx_scene_desc;
 
 /* Replaces the per-frame uniforms set in drawScene() (render.js:287-295).
@@ -177,6 +199,12 @@ int vx_scene_read_field(vx_scene *scene, void *host_out, size_t cap);
 int vx_scene_read_field_copy(vx_scene *scene, int octant, void *host_out, size_t cap);
 int vx_scene_read_boxes(vx_scene *scene, int octant, void *host_out, size_t cap);
 int vx_scene_dims(const vx_scene *scene, int dims[3]);
+/* The greedy mesh per face (ABI 8): 6 uint16 per cell, cell x fastest, normal
+ * index fastest within a cell (render.vert:14-17): du | dv << 8, the offset of
+ * the face from the origin of the quad covering it along the face's in-plane
+ * axes u = (d+1)%3, v = (d+2)%3 (d = normal index / 2); 0xFFFF where the mesh
+ * has no face.  The fragments' v_cellPos / v_fractPos split comes from it. */
+int vx_scene_read_face_quads(vx_scene *scene, void *host_out, size_t cap);
 /* The 2D mode mesh of the scene (what sdf.cpp:362-401 writes to
  * out/vertex2d.bin): the greedy quads of each column's top block (z >= 1) as
  * 16-byte vert2d records (sdf.cpp:154-173), six per quad.  out == NULL:

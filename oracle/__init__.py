@@ -24,7 +24,7 @@ class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
                 ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p),
                 ("exit_mode", C.c_int), ("held", C.c_void_p), ("held_oct", C.c_int), ("held_kx", C.c_int),
-                ("held_ky", C.c_int)]
+                ("held_ky", C.c_int), ("qoff", C.c_void_p), ("chunk", C.c_int)]
 
 
 class OStats(C.Structure):
@@ -44,7 +44,7 @@ class OMarch(C.Structure):
 
 class OGbuf(C.Structure):
     _fields_ = [("id", C.c_int), ("color", C.c_int), ("normal_idx", C.c_int), ("cell", C.c_int * 3),
-                ("fract", C.c_float * 3)]
+                ("fract", C.c_float * 3), ("t", C.c_float), ("key", C.c_uint64)]
 
 
 _lib = None
@@ -88,6 +88,13 @@ def lib():
         L.vxo_exit_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_int)]
         L.vxo_exit_plan.restype = C.c_int
+        L.vxo_face_quads.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.vxo_face_quads.restype = None
+        L.vxo_face_order.argtypes = [C.POINTER(C.c_int), C.c_int, C.c_uint16, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.vxo_face_order.restype = C.c_uint64
+        L.vxo_render_terms.argtypes = [C.POINTER(OScene), C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                       C.c_void_p, C.c_int]
+        L.vxo_render_terms.restype = None
         _lib = L
     return _lib
 
@@ -95,14 +102,23 @@ def lib():
 class Oracle:
     """Scalar restatement of render.frag over one field + noise texture."""
 
-    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_e=None, exit=False):
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_e=None, exit=False,
+                 quad=True, chunk: int = 0):
         """exit=False: the reference's literal march (every step of
         render.frag:92-136 counted).  exit=True: the build's sun exit tables
         (field_exit, chosen per frame by exit_plan) where the HIP kernel has
         them -- fields with Z <= 126 and every R, G <= Z (its padded int8 march
         copies) -- so the shadow fetch counters match the kernel's;
         exit="orthant": the orthant tables only (the kernel's VX_FLAG_NO_CONE).
-        Frames are identical in every mode."""
+        Frames are identical in every mode.
+
+        quad=True (default, as the kernel): the quad-relative G-buffer
+        (DESIGN.md §5): primary records carry the greedy quad's origin as
+        v_cellPos and the hit minus it as v_fractPos, as the raster hands them
+        to render.frag (render.vert:25-28; face_quads, the sdf.cpp:281-356
+        mesher with CHUNK = chunk or Z).  quad may also be a precomputed
+        face_quads() array; quad=False: the unit-cell split (the kernel's
+        VX_FLAG_UNIT_GBUF)."""
         self.field = np.ascontiguousarray(field_zyx4, np.uint8)
         self.noise = np.ascontiguousarray(noise_hw4, np.uint8)
         Z, Y, X, _ = self.field.shape
@@ -122,6 +138,13 @@ class Oracle:
             mode = 2 if exit == "orthant" else 1
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
                          (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data, mode)
+        self.qoff = None
+        if quad is not False and quad is not None:
+            self.qoff = (np.ascontiguousarray(quad, np.uint16) if isinstance(quad, np.ndarray)
+                         else face_quads(self.field, chunk))
+            assert self.qoff.shape == (Z, Y, X, 6)
+            self.sc.qoff = self.qoff.ctypes.data
+            self.sc.chunk = chunk
 
     def hold_exit_table(self, params):
         """Build the exit table the frame `params` reads (exit mode, every sample
@@ -145,6 +168,16 @@ class Oracle:
         lib().vxo_render(C.byref(self.sc), C.addressof(params), w, h, row0, row_step, out.ctypes.data,
                          C.byref(st), threads)
         return out, st
+
+    def terms(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0):
+        """Per pixel (h, w, 2): lit samples of the sun march of the first surface
+        (slot 0) and of what a glass pane blends over (slot 1), 255 = no march;
+        and sdf() of the AO sample (render.frag:223), NaN = none."""
+        lit = np.full((h, w, 2), 255, np.uint8)
+        amb = np.full((h, w, 2), np.nan, np.float32)
+        lib().vxo_render_terms(C.byref(self.sc), C.addressof(params), w, h, row0, row_step, lit.ctypes.data,
+                               amb.ctypes.data, threads)
+        return lit, amb
 
     def march(self, cell, fract, direction, max_steps=None):
         m = OMarch()
@@ -206,6 +239,17 @@ def footprint_2d(field_zyx4: np.ndarray) -> np.ndarray:
     for (x, y, w, h, col, _id) in mesh_ref.mesh2d(c2d):
         out[y:y + h, x:x + w, 1] = x | (y << 16)
     return np.ascontiguousarray(out)
+
+
+def face_quads(field_zyx4: np.ndarray, chunk: int = 0) -> np.ndarray:
+    """(Z, Y, X, 6) uint16: per cell and normal index, du | dv << 8 = the face's
+    offset from the origin of the greedy quad covering it (vxo_face_quads,
+    sdf.cpp:281-356 with CHUNK = chunk or Z); 0xFFFF where no face is."""
+    f = np.ascontiguousarray(field_zyx4, np.uint8)
+    Z, Y, X, _ = f.shape
+    out = np.empty((Z, Y, X, 6), np.uint16)
+    lib().vxo_face_quads(f.ctypes.data, X, Y, Z, int(chunk), out.ctypes.data)
+    return out
 
 
 def field_build(color_zyx: np.ndarray) -> np.ndarray:

@@ -47,6 +47,11 @@ typedef struct {
                                  held_ky}: a frame whose plan needs exactly that table reads it instead of
                                  building its own (the CPU baseline's timed frames); NULL = none */
     int held_oct, held_kx, held_ky;
+    const uint16_t *qoff;     /* quad-relative G-buffer: per cell and normal index, the offset
+                                 (du | dv << 8) of the face from its greedy quad's origin (vxo_face_quads); the
+                                 primary records then carry v_cellPos = the quad origin and v_fractPos = the hit
+                                 point minus it, as render.vert:25-28 hands them over.  NULL: the unit cell. */
+    int chunk;                /* the mesher's CHUNK (voxmap.h:9: Z); <= 0 -> Z */
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */
@@ -71,6 +76,14 @@ typedef struct {
 #define VXO_FLAG_REFLECT 0x10u  /* glass reflects the traced scene (README.md:15-20) */
 #define VXO_FLAG_ROUGH 0x20u    /* per-fragment normal jitter from white() (README.md:22, render.frag:21) */
 #define VXO_MAX_SAMPLES 16
+/* Glass in draw order: every front-facing glass face in front of
+ * the opaque surface is blended as the reference's raster does -- glass quads
+ * drawn after all opaque ones in vertex.bin order (sdf.cpp:284,337), depth test
+ * LESS with depth writes on, SRC_ALPHA blending (render.js:82-91) -- instead of
+ * the single layer.  Needs the quad table (vxo_scene.qoff).  Up to
+ * VXO_MAX_GLASS glass faces per pixel (the nearest ones) are blended. */
+#define VXO_FLAG_GLASS_ORDER 0x1000u
+#define VXO_MAX_GLASS 8
 
 typedef struct {
     uint64_t pixels, sky_px, block_px, glass_px;
@@ -99,6 +112,8 @@ typedef struct {
     int normal_idx;           /* 0..5 (render.vert:14-17) */
     int cell[3];              /* v_cellPos */
     float fract[3];           /* v_fractPos */
+    float t;                  /* ray parameter of the face (its depth along the view ray) */
+    uint64_t key;             /* glass faces: draw order of the covering quad (vxo_face_order) */
 } vxo_gbuf;
 
 /* Literal march() (render.frag:75-142). */
@@ -153,6 +168,23 @@ float vxo_exp2(float x);
  * a cell can show a face iff 1 <= B <= 21 ("vis colour" B, else 0). */
 #define VXO_PAL_SIZE 22
 static inline int vxo_vis(int b) { return (b >= 1 && b < VXO_PAL_SIZE) ? b : 0; }
+
+/* --- greedy mesh per face, vxo_mesh.c (sdf.cpp:281-356) ------------------ */
+#define VXO_NO_FACE 0xFFFFu
+/* out[6 * cell + nidx] = du | dv << 8: the offset, along the face's in-plane
+ * axes u = (d+1)%3 and v = (d+2)%3 (d = nidx / 2), of the face of `cell` with
+ * normal index nidx from the origin of the greedy quad covering it;
+ * VXO_NO_FACE where the mesh has no such face.  chunk <= 0 -> Z. */
+void vxo_face_quads(const uint8_t *rgba, int X, int Y, int Z, int chunk, uint16_t *out);
+/* Draw order (vertex.bin emission order) of the quad covering a face, for
+ * faces of one colour: smaller is drawn first. */
+uint64_t vxo_face_order(const int cell[3], int nidx, uint16_t off, int X, int Y, int Z, int chunk);
+/* Diagnostic: per pixel of rows row0::row_step, the sun-march result and AO
+ * distance of the first surface (slot 0) and of what a glass pane blends over
+ * (slot 1): lit[2*px + k] = lit samples (0/1 for the hard shadow), 255 = no
+ * march; amb[2*px + k] = sdf() of :223, NaN = no sample. */
+void vxo_render_terms(const vxo_scene *s, const vxo_frame *f, int w, int h, int row0, int row_step,
+                      uint8_t *lit, float *amb, int n_threads);
 
 /* --- field (map.bin) definition, vxo_field.c ---------------------------- */
 /* Build the RGBA8 field from a palette-index grid (x fastest), restating

@@ -324,7 +324,7 @@ static inline int in_grid(const vxo_scene *s, const int a[3]) {
  * the next change behind it (primary visibility); 0: the first change ends
  * the walk (reflection rays).  A start cell outside the grid is sky. */
 static int walk(const vxo_scene *s, const int cc[3], const float o[3], const float d[3], int c[3],
-                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit, int *glass_entries) {
+                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit, int *glass_entries, int quad) {
     const int dims[3] = {s->X, s->Y, s->Z};
     float inv[3];
     int stp[3];
@@ -371,22 +371,38 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
         OCT_E(abs_c, E);                           /* air box ahead */
         if (glass_entries && col == GLASS_INDEX && prev != GLASS_INDEX) (*glass_entries)++;
         /* a front face: entering a meshed cell from a cell of another colour
-         * (air is never meshed, sdf.cpp:229-233,284); with glass_layer the
+         * (air is never meshed, sdf.cpp:229-233,284); glass_layer 1: the
          * first glass entry is recorded and the walk goes on, later glass
-         * entries are not surfaces (one blend layer) */
-        if (col != prev && col != 0 && !(glass_layer && col == GLASS_INDEX && nrec == 1)) {
+         * entries are not surfaces (one blend layer); 2: every
+         * glass entry is recorded (up to VXO_MAX_GLASS, draw-order blending) */
+        if (col != prev && col != 0 && !(glass_layer == 1 && col == GLASS_INDEX && nrec == 1) &&
+            !(glass_layer == 2 && col == GLASS_INDEX && nrec >= VXO_MAX_GLASS)) {
             vxo_gbuf *h = &g[nrec];
             h->color = col;
             h->id = col == GLASS_INDEX ? 2 : 0;
             h->normal_idx = 2 * a + (stp[a] > 0 ? 1 : 0);
+            /* quad-relative G-buffer (render.vert:25-28): v_cellPos = the origin of
+             * the greedy quad covering the face, v_fractPos = the hit point minus
+             * it, rounded once (the unit cell's split rounds p - c the same way) */
+            int off[3] = {0, 0, 0};
+            uint16_t q = VXO_NO_FACE;
+            if (s->qoff)
+                q = s->qoff[6 * ((size_t)abs_c[0] + (size_t)s->X * ((size_t)abs_c[1] + (size_t)s->Y * (size_t)abs_c[2])) +
+                            (size_t)h->normal_idx];
+            if (quad && q != VXO_NO_FACE) {
+                off[(a + 1) % 3] = q & 0xff;
+                off[(a + 2) % 3] = q >> 8;
+            }
+            h->t = te;
+            h->key = q != VXO_NO_FACE ? vxo_face_order(abs_c, h->normal_idx, q, s->X, s->Y, s->Z, s->chunk) : 0;
             for (int i = 0; i < 3; i++) {
                 if (i == a) {
                     h->cell[i] = abs_c[i] + (stp[a] > 0 ? 0 : 1);
                     h->fract[i] = 0.0f;
                 } else {
                     float p = o[i] + te * d[i];
-                    h->cell[i] = abs_c[i];
-                    h->fract[i] = p - (float)c[i];
+                    h->cell[i] = abs_c[i] - off[i];
+                    h->fract[i] = p - (float)(c[i] - off[i]);
                 }
             }
             nrec++;
@@ -399,8 +415,8 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
 #undef OCT_E
 }
 
-int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
-                vxo_gbuf g[2], int *fetches, int *cap_hit) {
+static int primary_walk(const vxo_scene *s, const vxo_frame *f, const float d[3], int glass_layer, vxo_gbuf *g,
+                        int *fetches, int *cap_hit) {
     const int dims[3] = {s->X, s->Y, s->Z};
     const float *o = f->cam_fract;
     const int *cc = f->cam_cell;
@@ -429,7 +445,12 @@ int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
         int lo = -cc[i], hi = dims[i] - cc[i] - 1;
         c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
     }
-    return walk(s, cc, o, d, c, 1, g, fetches, cap_hit, NULL);
+    return walk(s, cc, o, d, c, glass_layer, g, fetches, cap_hit, NULL, 1);
+}
+
+int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
+                vxo_gbuf g[2], int *fetches, int *cap_hit) {
+    return primary_walk(s, f, d, 1, g, fetches, cap_hit);
 }
 
 /* Diagnostic (the single-layer glass deviation): per pixel, the
@@ -470,7 +491,7 @@ void vxo_glass_layers(const vxo_scene *s, const vxo_frame *f, int w, int h, uint
                     c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
                 }
                 vxo_gbuf g[2];       /* (the grid boundary has no faces: a glass start cell is no entry) */
-                walk(s, cc, o, d, c, 1, g, &fetches, &cap, &n);
+                walk(s, cc, o, d, c, 1, g, &fetches, &cap, &n, 0);
             }
             out[(size_t)py * w + px] = (uint8_t)(n > 255 ? 255 : n);
         }
@@ -559,6 +580,12 @@ static _Thread_local int g_rec_n, g_rec_cap;
 static inline void rec_march(int fetches) {
     if (g_rec && g_rec_n < g_rec_cap) g_rec[g_rec_n++] = fetches;
 }
+
+/* Diagnostic recorder (vxo_render_terms): the sun-march result and AO distance
+ * of the fragment being shaded into slot g_term_slot (-1 = none).  Thread-local. */
+static _Thread_local uint8_t *g_term_lit;
+static _Thread_local float *g_term_amb;
+static _Thread_local int g_term_slot = -1;
 
 /* Per-frame state derived once (the kernel's FrameConsts play this role). */
 typedef struct {
@@ -727,6 +754,7 @@ static void shade_frag(const shade_ctx *c, const vxo_gbuf *g, const float ray[3]
         int ac[3];
         for (int i = 0; i < 3; i++) ac[i] = g->cell[i] + g_f2i(v_normal[i]);
         float ambDist = sdf_lin(s, ac, g->fract);                                   /* :223 */
+        if (g_term_amb && g_term_slot >= 0) g_term_amb[g_term_slot] = ambDist;
         float ambFactor = g_min(1.0f - sqrtf(ambDist), 0.8f);                       /* :224 */
         for (int i = 0; i < 3; i++) ambCol[i] = g_mix(1.0f, shadeCol[i], ambFactor); /* :225 */
     }
@@ -748,7 +776,9 @@ static void shade_frag(const shade_ctx *c, const vxo_gbuf *g, const float ray[3]
                 rec_march(sun.fetches | (sun.step == c->max_steps ? 1 << 16 : 0));
             }
             shadeFactor = shadeFactor * ((float)lit / (float)c->n_sun);
+            if (g_term_lit && g_term_slot >= 0) g_term_lit[g_term_slot] = (uint8_t)lit;
         }
+        if (g_term_lit && g_term_slot >= 0 && c->n_sun <= 1) g_term_lit[g_term_slot] = sun.step == c->max_steps;
     }
     float lightCol[3];
     for (int i = 0; i < 3; i++) lightCol[i] = shadeCol[i] + litCol[i] * shadeFactor; /* :238 */
@@ -801,7 +831,7 @@ static void reflect_color(const shade_ctx *c, const vxo_gbuf *gl, const float rd
     }
     vxo_gbuf h[2];
     int fetches = 0, cap_hit = 0;
-    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit, NULL);
+    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit, NULL, 0);
     if (st) { st->reflect_rays++; st->reflect_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
     float rgba[4];
     if (n == 0) {
@@ -889,9 +919,10 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
         shade_2d(c, d, out, st);
         return;
     }
-    vxo_gbuf g[2];
+    vxo_gbuf g[VXO_MAX_GLASS + 1];
     int fetches = 0, cap_hit = 0;
-    int n = vxo_primary(s, f, d, g, &fetches, &cap_hit);
+    const int order = (f->flags & VXO_FLAG_GLASS_ORDER) && s->qoff;
+    int n = primary_walk(s, f, d, order ? 2 : 1, g, &fetches, &cap_hit);
     if (st) { st->pixels++; st->primary_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
     vxo_gbuf sky;
     sky_record(&sky);
@@ -904,13 +935,60 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
     if (n == 0) {
         if (st) st->sky_px++;
         shade_frag(c, &sky, d, out, NULL, st);
+    } else if (order && g[0].id == 2) {
+        /* the reference's raster: glass quads after every opaque one, in
+         * vertex.bin order; each passes the depth test (LESS, depth writes on)
+         * iff it is nearer than the last surface written, and blends over the
+         * colour there (render.js:82-91) */
+        if (st) st->glass_px++;
+        int ng = 0;
+        while (ng < n && g[ng].id == 2) ng++;
+        float dst[4], depth = INFINITY;
+        g_term_slot = 1;
+        if (ng < n) {
+            shade_frag(c, &g[ng], NULL, dst, NULL, st);
+            depth = g[ng].t;
+        } else {
+            shade_frag(c, &sky, d, dst, NULL, st);
+        }
+        g_term_slot = -1;
+        int idx[VXO_MAX_GLASS];
+        for (int k = 0; k < ng; k++) idx[k] = k;
+        for (int k = 1; k < ng; k++)          /* draw order (keys of distinct faces differ) */
+            for (int j = k; j > 0 && g[idx[j]].key < g[idx[j - 1]].key; j--) {
+                const int tmp = idx[j]; idx[j] = idx[j - 1]; idx[j - 1] = tmp;
+            }
+        for (int k = 0; k < ng; k++) {
+            const vxo_gbuf *gl = &g[idx[k]];
+            if (!(gl->t < depth)) continue;   /* behind the last surface written: fails LESS */
+            float src[4], rd[3];
+            g_term_slot = idx[k] == 0 ? 0 : -1;
+            shade_frag(c, gl, NULL, src, rd, st);
+            g_term_slot = -1;
+            if (f->flags & VXO_FLAG_REFLECT) {
+                float refl[3];
+                reflect_color(c, gl, rd, refl, st);
+                const float cs = g_min(fabsf(rd[gl->normal_idx >> 1]), 1.0f);
+                const float x = 1.0f - cs, x2 = x * x;
+                const float F = 0.04f + 0.96f * ((x2 * x2) * x);
+                for (int i = 0; i < 3; i++) src[i] = src[i] + F * refl[i];
+            }
+            const float a = src[3];
+            for (int i = 0; i < 3; i++) dst[i] = src[i] * a + dst[i] * (1.0f - a);
+            depth = gl->t;
+        }
+        out[0] = dst[0]; out[1] = dst[1]; out[2] = dst[2];
     } else if (g[0].id != 2) {
         if (st) st->block_px++;
+        g_term_slot = 0;
         shade_frag(c, &g[0], NULL, out, NULL, st);
+        g_term_slot = -1;
     } else {
         if (st) st->glass_px++;
         float src[4], dst[4], rd[3];
+        g_term_slot = 0;
         shade_frag(c, &g[0], NULL, src, rd, st);
+        g_term_slot = -1;
         if (f->flags & VXO_FLAG_REFLECT) {
             /* Schlick's Fresnel with F0 = 0.04 on the geometric normal:
              * cos = |rayDir| along the face axis */
@@ -921,8 +999,10 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
             const float F = 0.04f + 0.96f * ((x2 * x2) * x);
             for (int i = 0; i < 3; i++) src[i] = src[i] + F * refl[i];
         }
+        g_term_slot = 1;
         if (n == 2) shade_frag(c, &g[1], NULL, dst, NULL, st);
         else shade_frag(c, &sky, d, dst, NULL, st);
+        g_term_slot = -1;
         float a = src[3];
         for (int i = 0; i < 3; i++) out[i] = src[i] * a + dst[i] * (1.0f - a);
     }
@@ -984,5 +1064,34 @@ void vxo_march_lengths(const vxo_scene *s, const vxo_frame *f, int w, int h, int
             if (px0 + i < w && py0 + j < h) render_pixel(&ctx, w, h, px0 + i, py0 + j, rgba, NULL);
             g_rec = NULL;
         }
+    ctx_free(&ctx);
+}
+
+void vxo_render_terms(const vxo_scene *s, const vxo_frame *f, int w, int h, int row0, int row_step,
+                      uint8_t *lit, float *amb, int n_threads) {
+    if (row_step <= 0) row_step = 1;
+    const int nrows = row0 < h ? (h - 1 - row0) / row_step + 1 : 0;
+    shade_ctx ctx;
+    ctx_init(&ctx, s, f);
+    ctx_tables(&ctx);
+    (void)n_threads;
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads)
+#endif
+    for (int k = 0; k < nrows; k++) {
+        const int py = row0 + k * row_step;
+        for (int px = 0; px < w; px++) {
+            const size_t i = (size_t)py * w + px;
+            float rgba[4];
+            lit[2 * i] = lit[2 * i + 1] = 255;
+            amb[2 * i] = amb[2 * i + 1] = NAN;
+            g_term_lit = lit + 2 * i;
+            g_term_amb = amb + 2 * i;
+            render_pixel(&ctx, w, h, px, py, rgba, NULL);
+            g_term_lit = NULL;
+            g_term_amb = NULL;
+        }
+    }
     ctx_free(&ctx);
 }

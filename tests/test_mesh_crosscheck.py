@@ -101,7 +101,11 @@ def test_oracle_primary_matches_greedy_mesh(built, case):
             else:
                 q = quads[qi]
                 ours = np.array([rec.cell[i] + np.float64(rec.fract[i]) for i in range(3)])
+                # the record's v_cellPos is the quad's origin (render.vert:25: the
+                # vert() records carry it, sdf.cpp:94-102) and v_cellPos + v_fractPos
+                # the hit point
                 ok = (rec.color == q[9] and rec.normal_idx == q[10]
+                      and all(int(rec.cell[i]) == int(q[i]) for i in range(3))
                       and np.max(np.abs(ours - pt)) < 1e-3 * max(1.0, float(np.max(np.abs(pt)))))
             if not ok and len(bad) < 5:
                 bad.append((k, n, int(qi)))

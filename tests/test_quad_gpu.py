@@ -1,0 +1,148 @@
+"""The raster's G-buffer split on the GPU:
+the device's greedy mesh per face (k_face_quads) against the oracle's, and
+frames whose fragments carry the quad-relative split (the default) or the
+unit-cell one (VX_FLAG_UNIT_GBUF) against the oracle in the same mode, bit for
+bit, with every work counter -- on small scenes, the BASELINE C3 frame, the
+stacked-glass scene S-glass and a non-default mesh CHUNK."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(built):
+    try:
+        import torch
+        ok = torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        ok = False
+    if not ok:
+        pytest.skip("no GPU visible")
+
+
+def _scene(vx, field, noise, dims, **kw):
+    X, Y, Z = dims
+    return vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                    noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0, **kw)
+
+
+def _compare(img, ref):
+    bad = int(np.count_nonzero(img.view(np.uint32) != ref.view(np.uint32)))
+    if bad:
+        idx = np.argwhere(img.view(np.uint32) != ref.view(np.uint32))[:5]
+        raise AssertionError(f"{bad} words differ; first at {idx.tolist()}")
+
+
+def _counters_equal(st, ost):
+    g, o = st.as_dict(), ost.as_dict()
+    for k in o:
+        assert g[k] == o[k], (k, g[k], o[k])
+
+
+@pytest.mark.parametrize("seed,dims,chunk", [(0, (64, 32, 16), 0), (1, (70, 40, 16), 0), (2, (96, 48, 24), 8),
+                                             (3, (80, 40, 12), 40)])
+def test_face_table_matches_oracle_small(noise, seed, dims, chunk):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    field = vx.field_build(scenes.small_proc(seed, dims=dims, n_boxes=12, n_glass=4))
+    with _scene(vx, field, noise, dims, mesh_chunk=chunk) as sc:
+        q = sc.read_face_quads()
+    ref = oracle.face_quads(field, chunk)
+    assert (ref != 0xFFFF).sum() > 1000
+    assert np.array_equal(q, ref)
+
+
+@pytest.mark.parametrize("scene", ["s_proc", "s_glass", "s_up3"])
+def test_face_table_matches_oracle_baseline(scene):
+    """The BASELINE fields (C2-C4 S-proc, the stacked-glass fixture, C5's 3^3
+    field with CHUNK = Z = 96), built on the device from the palette grid."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid(scene)
+    Z, Y, X = grid.shape
+    with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, dims=(X, Y, Z), device=0) as sc:
+        field = sc.read_field(0)
+        q = sc.read_face_quads()
+    ref = oracle.face_quads(field)
+    assert np.array_equal(q, ref), int(np.count_nonzero(q != ref))
+
+
+SMALL = [
+    (5, (96, 48, 16), (48.0, 24.0, 18.0), (1.1, 0.0, 0.6)),
+    (11, (128, 64, 24), (-6.0, 32.0, 9.0), (1.45, 0.0, -1.5707963267948966)),
+    (13, (128, 64, 24), (64.0, 32.0, 6.0), (1.3, 0.0, 2.4)),
+]
+
+
+@pytest.mark.parametrize("quad", [True, False], ids=["quad", "unit"])
+@pytest.mark.parametrize("seed,dims,sbj,rot", SMALL)
+@pytest.mark.parametrize("flags,samples", [(0, 0), (48, 0), (48, 16), (48 | 0x80, 16), (48 | 0x100, 16)],
+                         ids=["v1", "full", "soft16", "soft16_pool", "soft16_brick"])
+def test_small_frames_both_splits(noise, seed, dims, sbj, rot, flags, samples, quad):
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    field = vx.field_build(scenes.small_proc(seed, dims=dims, n_boxes=16, n_glass=6))
+    f = flags | (0 if quad else vx.FLAG_UNIT_GBUF)
+    fr = vx.make_frame(sbj, rot, 160, 96, flags=f, shadow_samples=samples, sun_radius=0.04)
+    with _scene(vx, field, noise, dims) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True, quad=quad).render(fr.params, 160, 96)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+
+
+@pytest.mark.parametrize("flags", [0, 48], ids=["v1", "full"])
+def test_c3_unit_split_matches_oracle(noise, flags):
+    """The ABI <= 7 split on the bench's C3 frame (both kept exact)."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_proc"))
+    fr = presets.camera_frame("K1", 3840, 2160, flags=flags | vx.FLAG_UNIT_GBUF)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True, quad=False).render(fr.params, 3840, 2160, threads=16)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+
+
+@pytest.mark.parametrize("cam", ["K1", "K2"])
+def test_s_glass_c3_single_layer(noise, cam):
+    """S-glass (panes that stack along view rays), C3 full quality, the
+    single layer: every pixel and counter against the oracle."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid("s_glass")
+    field = vx.field_build(grid)
+    fr = presets.camera_frame(cam, 3840, 2160, flags=vx.FLAG_FULL_QUALITY)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 3840, 2160, threads=16)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+    assert st.glass_px > 100000
+
+
+def test_mesh_chunk_option(noise):
+    """A scene meshed with CHUNK 16 on a Z = 32 field: the device table and the
+    frames follow the option (VX scene_desc.mesh_chunk)."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (128, 64, 32)
+    field = vx.field_build(scenes.small_proc(21, dims=dims, n_boxes=20, n_glass=6))
+    fr = vx.make_frame((64.0, 32.0, 30.0), (1.1, 0.0, 0.6), 200, 120, flags=48)
+    with _scene(vx, field, noise, dims, mesh_chunk=16) as sc:
+        q = sc.read_face_quads()
+        img, st = sc.render(fr, stats=True)
+    ref_q = oracle.face_quads(field, 16)
+    assert np.array_equal(q, ref_q)
+    assert not np.array_equal(ref_q, oracle.face_quads(field, 0))
+    ref, ost = oracle.Oracle(field, noise, exit=True, quad=ref_q, chunk=16).render(fr.params, 200, 120)
+    _compare(img, ref)
+    _counters_equal(st, ost)

@@ -31,8 +31,12 @@ FLAG_SOFT_POOL = 0x80                           # soft shadows by the pooled wav
 FLAG_SOFT_BRICK = 0x100                         # + LDS 8^3 brick staging (same frames)
 FLAG_NO_EXIT = 0x200                            # diagnostics: march without the sun exit tables (same frames)
 FLAG_NO_CONE = 0x400                            # diagnostics: orthant exit tables only (same frames)
+FLAG_UNIT_GBUF = 0x800                          # diagnostics: the unit-cell G-buffer split (ABI <= 7)
+FLAG_GLASS_ORDER = 0x1000                       # every pane in draw order (render.js:82-91), not one layer
+FLAG_REFLECT_ALL = 0x2000                       # ext: every primary fragment mirrors the scene
+MAX_GLASS_LAYERS = 8
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 7
+ABI_VERSION = 8
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128
 
@@ -44,7 +48,7 @@ class SceneDesc(C.Structure):
         ("noise_path", C.c_char_p), ("noise_bytes", C.c_void_p), ("noise_size", C.c_size_t),
         ("noise_format", C.c_int), ("noise_w", C.c_int), ("noise_h", C.c_int),
         ("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int),
-        ("device", C.c_int), ("dist_cap", C.c_int), ("noise_seed", C.c_uint32),
+        ("device", C.c_int), ("dist_cap", C.c_int), ("noise_seed", C.c_uint32), ("mesh_chunk", C.c_int),
     ]
 
 
@@ -97,6 +101,7 @@ SIGNATURES = [
     ("vx_scene_read_field_copy", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("vx_scene_read_boxes", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("vx_scene_dims", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    ("vx_scene_read_face_quads", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("vx_scene_vertex2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("vx_render", C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_int, C.c_int, C.c_int,
                             C.c_void_p, C.c_int, C.c_void_p, C.POINTER(Stats)]),

@@ -45,6 +45,8 @@ struct vx_scene {
     uint16_t *d_rg = nullptr;     // R | G << 8
     uint32_t *d_rg2 = nullptr;    // AO x-pairs: (R, G) of cells x and x + 1, clamped, (X + 1) per row
     uint8_t *d_bcol = nullptr;    // map.bin's B channel as uploaded (vx_scene_read_field)
+    uint16_t *d_qface = nullptr;  // greedy mesh per face: 6 planes of X*Y*Z offsets from the quad origin
+    int chunk = 0;                // its CHUNK (sdf.cpp:284, voxmap.h:9)
     uint32_t *d_fp2d = nullptr;   // 2D mode: per column vis colour + quad corner (KernelArgs::fp2d)
     std::vector<Quad2d> quads2d;  // 2D mode: the footprint's greedy quads (vx_scene_vertex2d)
     uint32_t *d_noise = nullptr;
@@ -137,6 +139,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMalloc(&s->d_noise4, 4 * noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&s->d_bcol, field_bytes / 4)) != hipSuccess ||
+        (e = hipMalloc(&s->d_qface, 3 * field_bytes)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
         (!from_grid &&
          (e = hipMemcpyAsync(lin, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) ||
@@ -172,6 +175,8 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMemsetD32Async((hipDeviceptr_t)s->d_prim, 0xFFFFFFFF, 8 * L.texels, s->stream)) == hipSuccess) {
         // B -> vis colour first: the boxes and prim copies classify by it
         lrc = launch_field_vis(lin, s->d_bcol, X, Y, Z, s->stream);
+        // the greedy mesh's quad per face (render.vert:25-28: v_cellPos is the quad origin)
+        if (!lrc) lrc = launch_face_quads(lin, s->d_qface, X, Y, Z, in.chunk, s->stream);
         if (!lrc) lrc = build_2d(s, lin);
         if (!lrc) lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
         if (!lrc) lrc = launch_ao_pairs(s->d_rg, s->d_rg2, X, Y, Z, s->stream);
@@ -213,6 +218,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         return fail(set_error(VX_EDEVICE, std::string("field preparation failed: ") +
                                               hipGetErrorString(lrc ? (hipError_t)lrc : e)));
     s->L = L;
+    s->chunk = in.chunk;
     *out = s;
     return VX_OK;
 }
@@ -233,6 +239,7 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_rg2) (void)hipFree(s->d_rg2);
     if (s->d_noise4) (void)hipFree(s->d_noise4);
     if (s->d_bcol) (void)hipFree(s->d_bcol);
+    if (s->d_qface) (void)hipFree(s->d_qface);
     if (s->d_fp2d) (void)hipFree(s->d_fp2d);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
@@ -268,6 +275,21 @@ static int read_copy(vx_scene *s, int octant, void *host_out, size_t cap, bool b
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(lin);
     if (e != hipSuccess) return set_error(VX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    return VX_OK;
+}
+
+int vx_scene_read_face_quads(vx_scene *s, void *host_out, size_t cap) {
+    if (!s || !host_out) return set_error(VX_EINVAL, "vx_scene_read_face_quads: null argument");
+    const size_t N = (size_t)s->X * s->Y * s->Z;
+    if (cap < 12 * N) return set_error(VX_EINVAL, "vx_scene_read_face_quads: buffer too small");
+    VX_HIP(hipSetDevice(s->device));
+    uint16_t *tmp = nullptr;
+    VX_HIP(hipMalloc(&tmp, 12 * N));
+    hipError_t e = (hipError_t)launch_face_quads_interleave(s->d_qface, tmp, N, s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(host_out, tmp, 12 * N, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return set_error(VX_EDEVICE, std::string("vx_scene_read_face_quads: ") + hipGetErrorString(e));
     return VX_OK;
 }
 
@@ -398,6 +420,8 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.noise = s->d_noise;
     a.noise4 = s->d_noise4;
     a.fp2d = s->d_fp2d;
+    a.qface = s->d_qface;
+    a.quad_gbuf = (p->flags & VX_FLAG_UNIT_GBUF) ? 0 : 1;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;
     a.noise_w = s->noise_w; a.noise_h = s->noise_h;
     a.noise_rw = 1.0f / (float)s->noise_w;   // powers of two: exact

@@ -87,7 +87,17 @@ int vx::scene_inputs(const vx_scene_desc *d, SceneInputs &in) {
     // 32-bit buffer byte offsets and 24-bit index products in the kernels
     if (L.texels >= (1ull << 31) || (unsigned long long)L.Xp * L.Yp >= (1ull << 23))
         return set_error(VX_EINVAL, "vx_scene_create: field too large (padded grid must be < 2^31 cells)");
+    // the AO pair array (4 B per cell, X + 1 per row) and the noise quad planes
+    // (4 planes of 4 B per texel) are addressed with 32-bit byte offsets
+    if (4ull * ((unsigned long long)X + 1) * Y * Z >= (1ull << 32))
+        return set_error(VX_EINVAL, "vx_scene_create: field too large (4*(X+1)*Y*Z must be < 2^32)");
     if ((NW & (NW - 1)) || (NH & (NH - 1))) return set_error(VX_EINVAL, "noise dims must be powers of two");
+    if (16ull * (unsigned long long)NW * NH >= (1ull << 32))
+        return set_error(VX_EINVAL, "vx_scene_create: noise too large (16*w*h must be < 2^32)");
+    // CHUNK of the greedy mesh whose quads give the fragments' G-buffer split
+    // (voxmap.h:9: CHUNK = Z); offsets within a chunk are stored in 8 bits
+    const int chunk = d->mesh_chunk ? d->mesh_chunk : Z;
+    if (chunk < 1 || chunk > 255) return set_error(VX_EINVAL, "mesh_chunk must be in [1,255] (0: Z)");
     if (!!d->map_path == !!d->map_bytes) return set_error(VX_EINVAL, "set exactly one of map_path / map_bytes");
     const size_t field_bytes = (size_t)X * Y * Z * 4, noise_bytes = (size_t)NW * NH * 4;
 
@@ -123,7 +133,7 @@ int vx::scene_inputs(const vx_scene_desc *d, SceneInputs &in) {
         rc = noise_synth(d->noise_seed, NW, NH, noise.data());
         if (rc) return rc;
     }
-    in.X = X; in.Y = Y; in.Z = Z; in.NW = NW; in.NH = NH; in.cap = cap;
+    in.X = X; in.Y = Y; in.Z = Z; in.NW = NW; in.NH = NH; in.cap = cap; in.chunk = chunk;
     in.from_grid = from_grid;
     in.max_rg = max_rg;
     return VX_OK;

@@ -84,6 +84,8 @@ struct KernelArgs {
     const uint32_t *noise4;  // noise quads, planes A, R, G, B: entry (x, y) = that channel of (x, y), (x+1, y),
                              // (x, y+1), (x+1, y+1), REPEAT-wrapped
     const uint32_t *fp2d;    // 2D mode: 2 words per column (x fastest): vis colour, quad corner x0 | y0 << 16
+    const uint16_t *qface;   // greedy mesh per face: plane n (normal index) of X*Y*Z u16, du | dv << 8 (launch_face_quads)
+    int quad_gbuf;           // 1: fragments carry the quad-relative split (render.vert:25-28); 0: the unit cell
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
     float noise_rw, noise_rh;    // 1/noise_w, 1/noise_h (exact)
@@ -138,7 +140,7 @@ FieldLayout field_layout(int X, int Y, int Z, int cap);
 // vx_scene_create's host half (vx_host.cpp): the description checked, the map
 // and noise containers decoded and size-checked (or the noise synthesised).
 struct SceneInputs {
-    int X = 0, Y = 0, Z = 0, NW = 0, NH = 0, cap = 0;
+    int X = 0, Y = 0, Z = 0, NW = 0, NH = 0, cap = 0, chunk = 0;
     bool from_grid = false;           // VX_FORMAT_GRID: field holds nothing, the device builds it
     int max_rg = 0;                   // largest R/G of a decoded map.bin (march_pad needs <= Z)
     std::vector<unsigned char> field, noise;
@@ -162,6 +164,10 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
 // sample (all on the fast path, one sign pattern, r_z > 0, slopes <= 4, kx, ky
 // <= SB); 0 = each fast sample its octant's orthant copy (oracle vxo_exit_plan)
 int exit_plan(const FrameConsts &fc, int SB, int *oct, int *kx, int *ky);
+// the greedy mesh per face (sdf.cpp:281-356): 6 planes (normal index) of X*Y*Z u16, du | dv << 8 = the
+// face's offset from its quad's origin, 0xFFFF = no face; from the upload after launch_field_vis
+int launch_face_quads(const uint32_t *lin, uint16_t *qface, int X, int Y, int Z, int chunk, void *stream);
+int launch_face_quads_interleave(const uint16_t *qface, uint16_t *out, size_t N, void *stream);
 // AO x-pair array from rg: (X + 1) * Y * Z u32 (R, G of two x-neighbours, clamped)
 int launch_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z, void *stream);
 // noise quad texture from the RGBA8 noise: 4 planes (A, R, G, B) of each texel's wrapped 2x2 block

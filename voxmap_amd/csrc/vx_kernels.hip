@@ -576,7 +576,9 @@ __device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay 
 
 // The first step of a march from a face (DESIGN.md §3 "Sun exit tables", the
 // first step).  A fragment starts on its face plane (f = 0 on the face axis a)
-// with the in-face fracts f_j, f_k; when the sun lies on the face's normal
+// at in-face cells c_j + floor(f_j), c_k + floor(f_k) with fractions in
+// [0, 1) (RN(f + d) is monotone in d, so the step's cell moves by floor(f) +
+// 0 or 1 toward the sun on each in-face axis); when the sun lies on the face's normal
 // side, the first step -- len <= sqrt(3) * 1e-4/|r_a| (a tie takes the literal
 // length), so it moves under 0.2 cell on the other axes -- lands in the air
 // cell on the normal side or a neighbour of it toward the sun on the in-face
@@ -592,10 +594,14 @@ __device__ __forceinline__ bool first_step_exit(const KernelArgs &a, const int8_
     const int ax = g.nidx >> 1;
     const bool nneg = (g.nidx & 1) != 0;                   // face normal -e_a (render.vert:14-17)
     const bool spos = (sg >> ax) & 1;                      // sun toward +e_a
-    const float fj = ax == 0 ? g.f1 : g.f0, fk = ax == 2 ? g.f1 : g.f2;
+    // the in-face start: cell c + floor(f), fraction f - floor(f) (a quad-relative
+    // v_fractPos spans the quad: f up to CHUNK); a fraction that rounds to 1
+    // (f just below 0) fails the test and the samples march
+    const float fl0 = floorf(g.f0), fl1 = floorf(g.f1), fl2 = floorf(g.f2);
+    const float fj = ax == 0 ? g.f1 - fl1 : g.f0 - fl0, fk = ax == 2 ? g.f1 - fl1 : g.f2 - fl2;
     const bool ok = spos != nneg && fj >= 0.0f && fj < 1.0f && fk >= 0.0f && fk < 1.0f;
-    const int x = g.c0 - (ax == 0 && nneg ? 1 : 0), y = g.c1 - (ax == 1 && nneg ? 1 : 0),
-              z = g.c2 - (ax == 2 && nneg ? 1 : 0);
+    const int x = g.c0 + (ax == 0 ? (nneg ? -1 : 0) : (int)fl0), y = g.c1 + (ax == 1 ? (nneg ? -1 : 0) : (int)fl1),
+              z = g.c2 + (ax == 2 ? (nneg ? -1 : 0) : (int)fl2);
     // the air cell is inside the padded copy (a face lies inside the grid or on its edge)
     const unsigned off = (unsigned)(x + a.SB) + (unsigned)a.SXp * (unsigned)(y + a.SB) + a.SXpYp * (unsigned)(z + a.SB);
     const float v = ok ? ld_fmt1(buf_rsrc(ch, kRsrcS8), off) : 0.0f;
@@ -624,6 +630,21 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, i
     const uint8_t *ch = S.up ? a.sun : a.sun + a.XYZ;
     return S.fast ? march_fast(a, S, ch, c0, c1, c2, f0, f1, f2, cnt)
                   : march_literal(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
+}
+
+// The offset (per axis, as exact fp32 integers) of the face with normal index
+// nidx of cell (x, y, z) from the origin of the greedy quad covering it
+// (a.qface: du along u = (ax+1)%3, dv along v = (ax+2)%3, 0 on the face axis);
+// a cell without that face (never a primary hit) counts as its own origin,
+// as in the oracle.
+__device__ __forceinline__ void quad_offsets(const KernelArgs &a, int ax, int nidx, int x, int y, int z, float &o0,
+                                             float &o1, float &o2) {
+    unsigned q = a.qface[(size_t)nidx * a.XYZ + lin_index(a, x, y, z)];
+    q = q == 0xFFFFu ? 0u : q;
+    const float lo = (float)(q & 0xffu), hi = (float)(q >> 8);
+    o0 = ax == 2 ? lo : (ax == 1 ? hi : 0.0f);
+    o1 = ax == 0 ? lo : (ax == 2 ? hi : 0.0f);
+    o2 = ax == 1 ? lo : (ax == 0 ? hi : 0.0f);
 }
 
 // ---------------- primary visibility ----------------
@@ -775,15 +796,29 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     if (stop == 0) cnt.cap_hit++;
     const bool hit = stop != 0 && t < kSentinel;
     const int hax = tb0 == te ? 0 : (tb1 == te ? 1 : 2);    // exit axis of the last step (ties x < y < z)
-    // G-buffer records (v_cellPos on the face plane, v_fractPos, normal index)
+    // G-buffer records as the raster hands them over (render.vert:25-28):
+    // v_cellPos = the origin of the greedy quad covering the face (the face
+    // axis: its plane), v_fractPos = the hit point minus it, rounded once --
+    // p - (c - off) with c the entered cell and off its offset in the quad
+    // (a.qface; 0 with VX_FLAG_UNIT_GBUF: the unit cell's split p - c).  Both
+    // tables are read before either record is formed.
     int nrec = 0;
-    if (gmark != kGlass) {
-        const bool pos = gax == 0 ? p0 : (gax == 1 ? p1 : p2);
-        const int up = pos ? 0 : 1;
-        const float r0 = g0h - hp0, r1 = g1h - hp1, r2 = g2h - hp2;   // relative cell
+    const bool gl = gmark != kGlass;
+    const bool gpos = gax == 0 ? p0 : (gax == 1 ? p1 : p2);
+    const bool hpos = hax == 0 ? p0 : (hax == 1 ? p1 : p2);
+    const float gr0 = g0h - hp0, gr1 = g1h - hp1, gr2 = g2h - hp2;   // relative cells
+    const float hr0 = h0 - hp0, hr1 = h1 - hp1, hr2 = h2 - hp2;
+    float gq0 = 0.0f, gq1 = 0.0f, gq2 = 0.0f, hq0 = 0.0f, hq1 = 0.0f, hq2 = 0.0f;
+    if (a.quad_gbuf) {
+        if (gl) quad_offsets(a, gax, 2 * gax + (gpos ? 1 : 0), (int)gr0 + cc0, (int)gr1 + cc1, (int)gr2 + cc2, gq0, gq1, gq2);
+        if (hit) quad_offsets(a, hax, 2 * hax + (hpos ? 1 : 0), (int)hr0 + cc0, (int)hr1 + cc1, (int)hr2 + cc2, hq0, hq1, hq2);
+    }
+    if (gl) {
+        const int up = gpos ? 0 : 1;
+        const float r0 = gr0 - gq0, r1 = gr1 - gq1, r2 = gr2 - gq2;   // quad origin (exact small integers)
         g0.id = 2;
         g0.color = kGlass;
-        g0.nidx = 2 * gax + (pos ? 1 : 0);
+        g0.nidx = 2 * gax + (gpos ? 1 : 0);
         g0.c0 = (int)r0 + cc0 + (gax == 0 ? up : 0);
         g0.c1 = (int)r1 + cc1 + (gax == 1 ? up : 0);
         g0.c2 = (int)r2 + cc2 + (gax == 2 ? up : 0);
@@ -793,13 +828,12 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         nrec = 1;
     }
     if (hit) {
-        Surf &h = gmark != kGlass ? g1 : g0;
-        const bool pos = hax == 0 ? p0 : (hax == 1 ? p1 : p2);
-        const int up = pos ? 0 : 1;
-        const float r0 = h0 - hp0, r1 = h1 - hp1, r2 = h2 - hp2;
+        Surf &h = gl ? g1 : g0;
+        const int up = hpos ? 0 : 1;
+        const float r0 = hr0 - hq0, r1 = hr1 - hq1, r2 = hr2 - hq2;
         h.id = col == kGlass ? 2 : 0;
         h.color = (int)col;
-        h.nidx = 2 * hax + (pos ? 1 : 0);
+        h.nidx = 2 * hax + (hpos ? 1 : 0);
         h.c0 = (int)r0 + cc0 + (hax == 0 ? up : 0);
         h.c1 = (int)r1 + cc1 + (hax == 1 ? up : 0);
         h.c2 = (int)r2 + cc2 + (hax == 2 ? up : 0);
@@ -1466,7 +1500,9 @@ void k_render(KernelArgs a) {
                             const int d = lane + 64 * j, bi = d >> 7, row = (d & 127) >> 1, half = d & 1;
                             const int fb = min(base + bi, nf - 1);
                             const int4 pc = s_pc[wb + fb];
-                            const int ox = (pc.x + a.SB - bx) & ~3, oy = pc.y + a.SB - by, oz = pc.z + a.SB - bz;
+                            const float4 pf = s_pf[wb + fb];     // anchor: the start's unit cell c + floor(f)
+                            const int ox = (pc.x + (int)floorf(pf.x) + a.SB - bx) & ~3,
+                                      oy = pc.y + (int)floorf(pf.y) + a.SB - by, oz = pc.z + (int)floorf(pf.z) + a.SB - bz;
                             const size_t off = (size_t)(unsigned)ox + 4u * half +
                                                (size_t)(unsigned)a.SXp * (unsigned)(oy + (row & 7)) +
                                                (size_t)a.SXpYp * (unsigned)(oz + (row >> 3));
@@ -1483,7 +1519,8 @@ void k_render(KernelArgs a) {
                         if constexpr (kBrick) {
                             const int8_t *br = reinterpret_cast<const int8_t *>(s_brick + (wb >> 6) * 512) +
                                                512 * (lane >> lg);
-                            const int ox = (pc.x + a.SB - bx) & ~3, oy = pc.y + a.SB - by, oz = pc.z + a.SB - bz;
+                            const int ox = (pc.x + (int)floorf(pf.x) + a.SB - bx) & ~3,
+                                      oy = pc.y + (int)floorf(pf.y) + a.SB - by, oz = pc.z + (int)floorf(pf.z) + a.SB - bz;
                             switch (sgv) {
 #define VX_SGB(K) case K: lit = march_brick<K>(a, S, ch, br, ox, oy, oz, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
                                                cnt); break;
@@ -1851,6 +1888,89 @@ __global__ void k_oct_box(const uint32_t *lin, const int *S, uint32_t *dst, int 
     dst[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))] =
         col | ((uint32_t)e[0] << 8) | ((uint32_t)e[1] << 16) | ((uint32_t)e[2] << 24);
 }
+// ---- the greedy mesh per face (sdf.cpp:281-356; oracle vxo_face_quads): for
+// every face the mesh has, its offset du | dv << 8 from the origin of the quad
+// covering it, along u = (d+1)%3, v = (d+2)%3 -- the v_cellPos / v_fractPos
+// split the raster hands render.frag (render.vert:25-28).  One workgroup per
+// slice (chunk, d, normal, p[d] = 0 .. CH-1; the reference's slice -1 repeats
+// slice CH-1 of the chunk below, same cells, same quads): the lanes label the slice's
+// CH x CH mask in LDS (the face's colour, 0 = no face: normal 0 "cell is c, the
+// cell ahead along +d is not", normal 1 the reverse, ccol() clamping the
+// coordinates), then one lane runs the merge -- rows j outer, columns i inner,
+// width along u while the label holds, height along v while the whole row of w
+// holds, the quad's labels cleared (the reference clears its mask), the scan
+// going on at i + w.  Colours are disjoint, so the labelled slice yields
+// exactly the quads of the per-colour passes.  Positions past the grid (dims
+// not multiples of CH repeat the clamped edge cell) are not written.
+__global__ __launch_bounds__(64) void k_face_quads(const uint32_t *lin, uint16_t *qf, int X, int Y, int Z, int CH,
+                                                   int ncy, int ncz, size_t N) {
+    extern __shared__ uint8_t lab[];                       // CH * CH labels
+    __shared__ int any;
+    const int S = CH;                                      // slices p[d] = 0 .. CH-1 (-1 repeats the chunk below's CH-1)
+    const int pd = (int)(blockIdx.x % (unsigned)S);
+    const int normal = (int)((blockIdx.x / (unsigned)S) & 1u);
+    const int d = (int)((blockIdx.x / (unsigned)(2 * S)) % 3u);
+    const unsigned chunk = blockIdx.x / (unsigned)(6 * S);
+    const int base[3] = {(int)(chunk / (unsigned)(ncy * ncz)) * CH, (int)((chunk / (unsigned)ncz) % (unsigned)ncy) * CH,
+                         (int)(chunk % (unsigned)ncz) * CH};
+    const int u = d == 2 ? 0 : d + 1, v = d == 0 ? 2 : d - 1;
+    const int dims[3] = {X, Y, Z};
+    auto vis = [&](int p0, int p1, int p2) -> int {
+        p0 = min(max(p0, 0), X - 1); p1 = min(max(p1, 0), Y - 1); p2 = min(max(p2, 0), Z - 1);
+        return (int)((lin[(size_t)p0 + (size_t)X * ((size_t)p1 + (size_t)Y * (size_t)p2)] >> 16) & 0xffu);
+    };
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    int mine = 0;
+    for (int k = threadIdx.x; k < CH * CH; k += 64) {
+        const int j = k / CH, i = k % CH;
+        int p[3];
+        p[d] = base[d] + pd; p[u] = base[u] + i; p[v] = base[v] + j;
+        const int b = vis(p[0], p[1], p[2]);
+        p[d] += 1;
+        const int a = vis(p[0], p[1], p[2]);
+        int l = 0;
+        if (normal == 0 && b != 0 && a != b) l = b;
+        if (normal == 1 && a != 0 && b != a) l = a;
+        lab[k] = (uint8_t)l;
+        mine |= l;
+    }
+    if (mine) any = 1;
+    __syncthreads();
+    if (!any || threadIdx.x != 0) return;
+    for (int j = 0; j < CH; j++)
+        for (int i = 0; i < CH; i++) {
+            const int c = lab[j * CH + i];
+            if (!c) continue;
+            int w = 1, h = 1;
+            while (i + w < CH && lab[j * CH + i + w] == c) w++;
+            for (; j + h < CH; h++) {
+                bool ok = true;
+                for (int k = 0; k < w && ok; k++) ok = lab[(j + h) * CH + i + k] == c;
+                if (!ok) break;
+            }
+            for (int l = 0; l < h; l++)
+                for (int k = 0; k < w; k++) {
+                    lab[(j + l) * CH + i + k] = 0;
+                    int cell[3];
+                    cell[d] = base[d] + pd + normal;
+                    cell[u] = base[u] + i + k;
+                    cell[v] = base[v] + j + l;
+                    if (cell[0] < 0 || cell[1] < 0 || cell[2] < 0 || cell[0] >= dims[0] || cell[1] >= dims[1] ||
+                        cell[2] >= dims[2])
+                        continue;
+                    const size_t ci = (size_t)cell[0] + (size_t)X * ((size_t)cell[1] + (size_t)Y * (size_t)cell[2]);
+                    qf[(size_t)(2 * d + normal) * N + ci] = (uint16_t)(k | (l << 8));
+                }
+            i += w - 1;
+        }
+}
+// the table in the oracle's layout (6 per cell) for vx_scene_read_face_quads
+__global__ void k_face_quads_interleave(const uint16_t *qf, uint16_t *out, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 6 * N) return;
+    out[i] = qf[(i % 6) * N + i / 6];
+}
 // AO x-pairs (sdf_lin): entry (p, y, z), p = 0..X, = rg of cells clamp(p - 1) and clamp(p)
 __global__ void k_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2036,6 +2156,25 @@ int launch_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z, void
     const size_t N = ((size_t)X + 1) * Y * Z;
     hipLaunchKernelGGL(k_ao_pairs, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rg, rg2, X, Y,
                        Z);
+    return (int)hipGetLastError();
+}
+
+int launch_face_quads(const uint32_t *lin, uint16_t *qface, int X, int Y, int Z, int chunk, void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(qface, 0xFF, 12 * N, s);
+    if (e != hipSuccess) return (int)e;
+    const int ncx = (X + chunk - 1) / chunk, ncy = (Y + chunk - 1) / chunk, ncz = (Z + chunk - 1) / chunk;
+    const size_t blocks = (size_t)ncx * ncy * ncz * 6 * chunk;
+    if (blocks >= (1ull << 31)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_face_quads, dim3((unsigned)blocks), dim3(64), (size_t)chunk * chunk, s, lin, qface, X, Y, Z,
+                       chunk, ncy, ncz, N);
+    return (int)hipGetLastError();
+}
+
+int launch_face_quads_interleave(const uint16_t *qface, uint16_t *out, size_t N, void *stream) {
+    hipLaunchKernelGGL(k_face_quads_interleave, dim3((unsigned)((6 * N + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, qface, out, N);
     return (int)hipGetLastError();
 }
 

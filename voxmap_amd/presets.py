@@ -44,6 +44,8 @@ def camera_frame(name: str, w: int, h: int, scale: float = 1.0, **kw):
 def scene_grid(name: str, seed: int = 1):
     if name == "s_proc":
         return scenes.s_proc(seed)
+    if name == "s_glass":
+        return scenes.s_glass(seed)
     if name == "s_campus":
         return scenes.s_campus()
     if name == "s_up3":

@@ -96,7 +96,7 @@ class Scene:
 
     def __init__(self, *, map_path=None, map_bytes=None, map_format=_abi.FORMAT_AUTO, key=None,
                  noise_path=None, noise_bytes=None, noise_format=_abi.FORMAT_AUTO, noise_size=(1024, 1024),
-                 dims=DEFAULT_DIMS, device=0, dist_cap=32, noise_seed=0):
+                 dims=DEFAULT_DIMS, device=0, dist_cap=32, noise_seed=0, mesh_chunk=0):
         L = lib()
         d = _abi.SceneDesc()
         self._keep = []
@@ -123,6 +123,7 @@ class Scene:
         d.device = int(device)
         d.dist_cap = int(dist_cap)
         d.noise_seed = int(noise_seed)
+        d.mesh_chunk = int(mesh_chunk)
         h = C.c_void_p()
         check(L.vx_scene_create(C.byref(d), C.byref(h)))
         self._h = h
@@ -167,6 +168,14 @@ class Scene:
         out = np.empty(n.value, np.uint8)
         check(lib().vx_scene_vertex2d(self.handle, out.ctypes.data, out.size, C.byref(n)))
         return out.tobytes()
+
+    def read_face_quads(self) -> np.ndarray:
+        """(Z, Y, X, 6) uint16: per cell and normal index, the face's offset du | dv << 8
+        from the origin of its greedy quad (vx_scene_read_face_quads); 0xFFFF = no face."""
+        X, Y, Z = self.dims
+        out = np.empty((Z, Y, X, 6), np.uint16)
+        check(lib().vx_scene_read_face_quads(self.handle, out.ctypes.data, out.nbytes))
+        return out
 
     def read_boxes(self, octant: int = 0) -> np.ndarray:
         """(Z, Y, X, 4) uint8: colour, ex, ey, ez of the octant's traversal boxes."""

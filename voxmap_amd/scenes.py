@@ -101,6 +101,31 @@ def upsample3(g: np.ndarray, k: int = 3) -> np.ndarray:
     return np.repeat(np.repeat(np.repeat(g, k, axis=0), k, axis=1), k, axis=2)
 
 
+def s_glass(seed: int = 1, dims=(1024, 256, 32), n_houses: int = 60, n_facades: int = 40) -> np.ndarray:
+    """S-glass: S-proc plus glass that stacks along a view ray (the
+    single-layer deviation): hollow glass pavilions (a one-voxel glass shell
+    around air: a ray crosses the front pane, then the inside of the back pane,
+    both front-facing glass faces) and glass screens standing off two facades of
+    a building.  Deterministic in ``seed``."""
+    X, Y, Z = dims
+    g = s_proc(seed, dims)
+    rng = np.random.default_rng(seed + 1000)
+    for _ in range(n_houses):                  # hollow glass pavilions on the ground
+        w = int(rng.integers(6, 24)); d = int(rng.integers(6, 24)); hgt = int(rng.integers(4, min(16, Z - 2)))
+        x0 = int(rng.integers(0, X - w)); y0 = int(rng.integers(0, Y - d))
+        g[1:1 + hgt, y0:y0 + d, x0:x0 + w] = GLASS
+        g[1:hgt, y0 + 1:y0 + d - 1, x0 + 1:x0 + w - 1] = 0          # open inside, glass roof kept
+    for _ in range(n_facades):                 # a building with glass screens off two facades
+        w = int(rng.integers(8, 30)); d = int(rng.integers(8, 30)); hgt = int(rng.integers(6, min(24, Z - 1)))
+        x0 = int(rng.integers(4, X - w - 4)); y0 = int(rng.integers(4, Y - d - 4))
+        col = int(rng.integers(1, 21))
+        g[1:1 + hgt, y0:y0 + d, x0:x0 + w] = col
+        off = int(rng.integers(2, 4))
+        g[1:1 + hgt, y0 - off, x0:x0 + w] = GLASS                  # screen in front of the -y facade
+        g[1:1 + hgt, y0:y0 + d, x0 + w - 1 + off] = GLASS          # and of the +x facade
+    return g
+
+
 def single_block(dims=(64, 32, 16), at=(20, 12, 1), color=5) -> np.ndarray:
     X, Y, Z = dims
     g = np.zeros((Z, Y, X), np.uint8)
