@@ -120,9 +120,13 @@ def spawn_ranks(n: int, argv) -> int:
 
 
 # ---------------------------------------------------------------- timing
-def timed(sync, step, steps, warmup, settle_ms, dist=None, sync_dev=None):
-    """Settle the clock, warm up, then time `steps` frames bracketed by a barrier
-    and a device synchronise on both sides (max over ranks taken by the caller)."""
+REPEATS = 7             # timed blocks of `steps` frames each; the line reports their median
+
+
+def timed(sync, step, steps, warmup, settle_ms, dist=None, sync_dev=None, repeats=1):
+    """Settle the clock, warm up, then time `repeats` blocks of exactly `steps`
+    frames, each bracketed by a barrier and a device synchronise on both sides
+    (max over ranks taken by the caller).  Returns the blocks' wall times (s)."""
     import torch
     settle = 0
     if settle_ms > 0:
@@ -142,18 +146,31 @@ def timed(sync, step, steps, warmup, settle_ms, dist=None, sync_dev=None):
             step()
     for _ in range(warmup):
         step()
-    sync()
-    if dist is not None:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    sync()
-    if dist is not None:
-        dist.barrier()
-    sync()
-    return time.perf_counter() - t0, settle
+    walls = []
+    for _ in range(max(1, repeats)):
+        sync()
+        if dist is not None:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        sync()
+        if dist is not None:
+            dist.barrier()
+        sync()
+        walls.append(time.perf_counter() - t0)
+    return walls, settle
+
+
+def block_summary(walls, steps):
+    """Median block time and the spread of the timed blocks (the line's ms_per_step is the median)."""
+    ms = sorted(1000.0 * w / steps for w in walls)
+    med = ms[len(ms) // 2] if len(ms) % 2 else 0.5 * (ms[len(ms) // 2 - 1] + ms[len(ms) // 2])
+    return med, {"blocks": len(ms), "steps_per_block": steps, "ms_per_step_blocks": [round(v, 4) for v in ms],
+                 "median_ms_per_step": round(med, 4), "spread_pct": round(100.0 * (ms[-1] - ms[0]) / med, 2),
+                 "how": "each block: exactly `steps` frames between a barrier + device synchronise on both sides; "
+                        "value and ms_per_step from the median block"}
 
 
 def event_ms(torch, one, steps):
@@ -208,7 +225,7 @@ def exit_tables(torch, vx, scene, frame, W, H):
     return info
 
 
-def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms):
+def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms, repeats=REPEATS):
     """N = 1: K frames in flight over K streams/framebuffers; timings + stats."""
     ex = exit_tables(torch, vx, scene, frame, W, H)
     streams = [torch.cuda.Stream() for _ in range(K)]
@@ -223,9 +240,11 @@ def single_gpu(torch, vx, scene, frame, W, H, K, steps, warmup, settle_ms):
     def step():
         fns[n[0] % K]()
         n[0] += 1
-    wall, settle = timed(torch.cuda.synchronize, step, steps, warmup, settle_ms)
-    ev = event_ms(torch, fns[0], steps)
-    return {"wall_s": wall, "settle": settle, "ev_ms": ev, "stats": st.as_dict(), "exit": ex}
+    walls, settle = timed(torch.cuda.synchronize, step, steps, warmup, settle_ms, repeats=repeats)
+    med, blocks = block_summary(walls, steps)
+    ev = sorted(event_ms(torch, fns[0], steps) for _ in range(3))[1]
+    return {"wall_s": med * steps / 1000.0, "blocks": blocks, "settle": settle, "ev_ms": ev, "stats": st.as_dict(),
+            "exit": ex}
 
 
 def fps_with_d2h(torch, vx, scene, frame, W, H, frames, K=2):
@@ -383,13 +402,14 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
     def step():
         fns[n[0] % K]()
         n[0] += 1
-    wall, settle_steps = timed(sync, step, args.steps, args.warmup, 0.0 if standin else args.settle_ms, dist,
-                               "cuda" if on_dev else None)
-    tt = torch.tensor([wall], dtype=torch.float64)
+    walls, settle_steps = timed(sync, step, args.steps, args.warmup, 0.0 if standin else args.settle_ms, dist,
+                                "cuda" if on_dev else None, repeats=REPEATS)
+    tt = torch.tensor(walls, dtype=torch.float64)
     if on_dev:
         tt = tt.cuda()
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    wall = float(tt.item())
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)             # per block, the slowest rank
+    med, blocks = block_summary([float(v) for v in tt.cpu().tolist()], args.steps)
+    wall = med * args.steps / 1000.0
     if rank == 0 and standin:
         # the gathered frame must hold every band's stand-in value
         from voxmap_amd.dist import band_rows_of as bro
@@ -413,7 +433,7 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
                 mg.gather(W, H, BAND, frames[0].data_ptr(), stream=s0)
             tr, _ = timed(sync, r_only, args.steps, 2, 0.0, dist)
             tg, _ = timed(sync, g_only, args.steps, 2, 0.0, dist)
-            t2 = torch.tensor([tr, tg], dtype=torch.float64)
+            t2 = torch.tensor([tr[0], tg[0]], dtype=torch.float64)
             dist.all_reduce(t2, op=dist.ReduceOp.MAX)
             split_ms = {"render_ms": round(1000.0 * float(t2[0]) / args.steps, 4),
                         "gather_ms": round(1000.0 * float(t2[1]) / args.steps, 4),
@@ -425,7 +445,7 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
         mg.close()
     shards = {"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
               "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc, "split_ms": split_ms}
-    return stats, wall, settle_steps, shards
+    return stats, wall, settle_steps, shards, blocks
 
 
 # ---------------------------------------------------------------- main
@@ -492,10 +512,10 @@ def main(argv=None):
     if world == 1:
         r = single_gpu(torch, vx, scene, frame, W, H, K, args.steps, args.warmup, args.settle_ms)
         stats, wall, settle_steps, ev_ms = r["stats"], r["wall_s"], r["settle"], r["ev_ms"]
-        exit_info = r["exit"]
+        exit_info, blocks = r["exit"], r["blocks"]
     else:
-        stats, wall, settle_steps, shards = multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world,
-                                                       local, standin)
+        stats, wall, settle_steps, shards, blocks = multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank,
+                                                               world, local, standin)
         ev_ms = None
     ms_per_step = 1000.0 * wall / args.steps
 
@@ -504,7 +524,7 @@ def main(argv=None):
         # the reference's own shader (v1, flags 0) on the same frame: the same
         # K-in-flight wall timing, and one stream with events for its roofline
         fr1 = presets.camera_frame(cam, W, H, scale=up)
-        a = single_gpu(torch, vx, scene, fr1, W, H, K, args.steps, args.warmup, 0.0)
+        a = single_gpu(torch, vx, scene, fr1, W, H, K, args.steps, args.warmup, 0.0, repeats=3)
         s1 = a["stats"]
         r1 = s1["pixels"] + s1["shadow_rays"]
         ms1w = 1000.0 * a["wall_s"] / args.steps
@@ -527,22 +547,42 @@ def main(argv=None):
         f5 = presets.camera_frame(c5cfg["camera"], c5cfg["w"], c5cfg["h"], scale=3.0, flags=flags,
                                   shadow_samples=c5cfg["samples"], sun_radius=args.sun_radius)
         n5 = max(10, args.steps // 5)
-        b = single_gpu(torch, vx, sc5, f5, c5cfg["w"], c5cfg["h"], K, n5, 3, 100.0)
+        b = single_gpu(torch, vx, sc5, f5, c5cfg["w"], c5cfg["h"], K, n5, 3, 100.0, repeats=3)
         s5 = b["stats"]
         rays5 = s5["pixels"] + s5["shadow_rays"] + s5["reflect_rays"]
+        marched5 = rays5 - s5["shadow_rays_resolved"]
         ms5 = 1000.0 * b["wall_s"] / n5
         ach5, frac5 = roofline_of(s5["alg_bytes"], b["ev_ms"])
-        t5j = pmc_entry("traffic_r03_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
+        t5j = pmc_entry("traffic_r04_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
         c5 = {"workload": f"C5: {c5cfg['w']}x{c5cfg['h']}, field {X5}x{Y5}x{Z5} (S-proc 3x nearest upsample), "
                           f"full quality + {c5cfg['samples']}-sample soft shadows (sun radius {args.sun_radius})",
-              "ms_per_frame": round(ms5, 4), "mrays_per_s": round(rays5 / ms5 / 1e3, 3), "fps": round(1000 / ms5, 2),
-              "rays_per_frame": int(rays5), "single_stream_ms_per_frame": round(b["ev_ms"], 4),
+              "ms_per_frame": round(ms5, 4), "fps": round(1000 / ms5, 2),
+              # a soft-shadowed fragment whose first step lands in a marked exit-table block
+              # resolves all its samples by one table test: those rays are
+              # resolved, not marched
+              "mrays_per_s_resolved": round(rays5 / ms5 / 1e3, 3), "rays_resolved_per_frame": int(rays5),
+              "mrays_per_s_marched": round(marched5 / ms5 / 1e3, 3), "rays_marched_per_frame": int(marched5),
+              "single_stream_ms_per_frame": round(b["ev_ms"], 4),
               "alg_bytes": int(s5["alg_bytes"]), "roofline_achieved_gbps": round(ach5, 2),
               "roofline_frac": round(frac5, 4), "traffic": t5j.get("hbm_bytes_per_launch") if t5j else None,
-              "lane_util": lane_utils(s5), "scene_build_s": round(t5, 3), "frames": n5,
-              "exit_tables": b["exit"],
-              "reference_alg_frac": round(roofline_of(b["exit"]["reference_alg_bytes"], b["ev_ms"])[1], 4)}
+              "lane_util": lane_utils(s5), "scene_build_s": round(t5, 3), "frames": n5, "timing": b["blocks"],
+              "exit_tables": b["exit"]}
         sc5.close()
+    c3ra = None
+    if world == 1 and cfg_name == "C3" and flags == vx.FLAG_FULL_QUALITY and args.flags is None and samples <= 1:
+        # a reflection workload over the whole frame -- every first
+        # surface traces its mirror ray (VX_FLAG_REFLECT_ALL), next to the headline
+        fra = presets.camera_frame(cam, W, H, scale=up, flags=flags | vx.FLAG_REFLECT_ALL)
+        c = single_gpu(torch, vx, scene, fra, W, H, K, args.steps, args.warmup, 0.0, repeats=3)
+        sr = c["stats"]
+        rr = sr["pixels"] + sr["shadow_rays"] + sr["reflect_rays"]
+        msr = 1000.0 * c["wall_s"] / args.steps
+        c3ra = {"workload": "C3 full quality + VX_FLAG_REFLECT_ALL (every first surface mirrors the traced scene, "
+                            "Schlick-weighted; DESIGN.md §3 Extensions)",
+                "ms_per_frame": round(msr, 4), "mrays_per_s": round(rr / msr / 1e3, 3), "rays_per_frame": int(rr),
+                "reflect_rays": int(sr["reflect_rays"]), "single_stream_ms_per_frame": round(c["ev_ms"], 4),
+                "alg_bytes": int(sr["alg_bytes"]), "roofline_frac": round(roofline_of(sr["alg_bytes"], c["ev_ms"])[1], 4),
+                "timing": c["blocks"]}
 
     rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
     value = rays * args.steps / wall / 1e6                                   # whole-job Mrays/s
@@ -551,7 +591,7 @@ def main(argv=None):
         per_launch_bytes = float(stats["alg_bytes"]) / world if world > 1 else float(stats["alg_bytes"])
         kernel_ms = ev_ms if world == 1 else stats["kernel_ms"]
         achieved, frac = roofline_of(per_launch_bytes, kernel_ms) if kernel_ms else (0.0, 0.0)
-        tag = "r03" if cfg_name != "C5" else "r03_c5"
+        tag = "r04" if cfg_name != "C5" else "r04_c5"
         traffic = pmc_entry(f"traffic_{tag}.json", cfg_name, cam, flags, samples) if world == 1 else None
         valu = pmc_entry(f"valu_{tag}.json", cfg_name, cam, flags, samples) if world == 1 else None
         if valu is None and not standin:
@@ -559,7 +599,7 @@ def main(argv=None):
             # every rank of N > 1 run the C3 kernel; soft shadows the C5 one)
             ref_cfg = "C5" if samples > 1 else "C3"
             c_ref = presets.CONFIGS[ref_cfg]
-            valu = pmc_entry(f"valu_r03{'_c5' if samples > 1 else ''}.json", ref_cfg, c_ref["camera"], flags,
+            valu = pmc_entry(f"valu_r04{'_c5' if samples > 1 else ''}.json", ref_cfg, c_ref["camera"], flags,
                              c_ref.get("samples", 1) if samples > 1 else 1)
             if valu is not None:
                 valu = dict(valu, source=f"{valu.get('source', '')}; measured on {ref_cfg}, the same kernel "
@@ -594,6 +634,7 @@ def main(argv=None):
                              f"each step, {K} frames in flight"),
                 "flags": flags, "shadow_samples": samples, "scene_build_s": round(t_scene, 3),
                 "clock_settle": {"ms": args.settle_ms, "untimed_frames": settle_steps},
+                "timing": blocks,
                 "width": W, "height": H, "field": [X, Y, Z], "camera": cam,
                 "shards": shards,
                 "fps": round(1000.0 / ms_per_step, 2),
@@ -607,6 +648,13 @@ def main(argv=None):
                 "mrays_per_s_nominal_2rpp": round(2 * stats["pixels"] * args.steps / wall / 1e6, 3),
                 "v1": v1,
                 "c5": c5,
+                "c3_reflect_all": c3ra,
+                # not a roofline fraction: the reference's march takes every step of
+                # render.frag:92-136 (VX_FLAG_NO_EXIT); the build's exit tables skip the
+                # steps of marches that can no longer end unlit.  Work ratio of the same
+                # frame in SURVEY §8d bytes (reference / this build); C5's is in c5.exit_tables.
+                "reference_work_ratio": (round(exit_info["reference_alg_bytes"] / max(1, stats["alg_bytes"]), 4)
+                                         if exit_info else None),
             },
             "roofline": {
                 # achieved/peak/frac: the contract's unit, algorithmic bytes
@@ -623,12 +671,6 @@ def main(argv=None):
                 "frac": round(frac, 4),
                 "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
                 "alg_bytes_per_launch": int(per_launch_bytes),
-                # the same formula over the reference's own step count (every march
-                # step of render.frag:92-136, VX_FLAG_NO_EXIT): what the launch
-                # computes, in the reference algorithm's bytes
-                "reference_alg_bytes_per_launch": exit_info["reference_alg_bytes"] if exit_info else None,
-                "reference_alg_frac": (round(roofline_of(exit_info["reference_alg_bytes"], kernel_ms)[1], 4)
-                                       if exit_info and kernel_ms else None),
                 "avg_launch_ms": round(kernel_ms, 4) if kernel_ms else None,
                 "fabric_gbps": (round(traffic["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 1)
                                 if traffic else None),

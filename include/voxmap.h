@@ -110,10 +110,11 @@ extern "C" {
  * The nearest VX_MAX_GLASS_LAYERS panes of a pixel take part. */
 #define VX_FLAG_GLASS_ORDER 0x1000u
 #define VX_MAX_GLASS_LAYERS 8
-/* Extension (ABI 8): every primary fragment mirrors the traced scene, as
- * VX_FLAG_REFLECT does for glass: the first surface (and what a pane blends
- * over) adds Schlick F * the colour along its mirror ray (DESIGN.md §3
- * "Extensions"; README.md:18-25 describes a reflection pass over the frame). */
+/* Extension (ABI 8): every first surface mirrors the traced scene, as
+ * VX_FLAG_REFLECT does for glass: the surface a pixel shows first (and every
+ * pane blended in draw order) adds Schlick F * the colour along its mirror ray
+ * (DESIGN.md §3 "Extensions"; README.md:18-25 describes a reflection pass over
+ * the frame).  What a pane blends over is seen through the glass: not mirrored. */
 #define VX_FLAG_REFLECT_ALL 0x2000u
 #define VX_MAX_SHADOW_SAMPLES 16
 
@@ -180,6 +181,10 @@ typedef struct vx_stats {
     uint64_t march_lane_slots;  /* diagnostic (ABI 6): per march wave iteration, the lanes that
                                    began that march; shadow_fetches / march_lane_slots = the
                                    utilisation of the marching lanes alone */
+    uint64_t shadow_rays_resolved;   /* diagnostic (ABI 8): shadow rays counted in shadow_rays whose lit
+                                   flag came from one exit-table test of the fragment's first step
+                                   instead of a march (soft shadows): rays resolved, not
+                                   marched; shadow_rays - this = rays marched */
     uint64_t alg_bytes;         /* 4*(primary+shadow+reflect fetches) + 32*ao + 80*clouded sky
                                    + 16*rough + out bytes */
     double kernel_ms;           /* HIP-event time of the render kernel(s) */

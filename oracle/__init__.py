@@ -24,7 +24,7 @@ class OScene(C.Structure):
     _fields_ = [("X", C.c_int), ("Y", C.c_int), ("Z", C.c_int), ("field", C.c_void_p), ("noise", C.c_void_p),
                 ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p),
                 ("exit_mode", C.c_int), ("held", C.c_void_p), ("held_oct", C.c_int), ("held_kx", C.c_int),
-                ("held_ky", C.c_int), ("qoff", C.c_void_p), ("chunk", C.c_int)]
+                ("held_ky", C.c_int), ("qoff", C.c_void_p), ("chunk", C.c_int), ("unit_split", C.c_int)]
 
 
 class OStats(C.Structure):
@@ -138,13 +138,13 @@ class Oracle:
             mode = 2 if exit == "orthant" else 1
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
                          (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data, mode)
-        self.qoff = None
-        if quad is not False and quad is not None:
-            self.qoff = (np.ascontiguousarray(quad, np.uint16) if isinstance(quad, np.ndarray)
-                         else face_quads(self.field, chunk))
-            assert self.qoff.shape == (Z, Y, X, 6)
-            self.sc.qoff = self.qoff.ctypes.data
-            self.sc.chunk = chunk
+        # the quad table serves the split and the glass draw order (VX_FLAG_GLASS_ORDER)
+        self.qoff = (np.ascontiguousarray(quad, np.uint16) if isinstance(quad, np.ndarray)
+                     else face_quads(self.field, chunk))
+        assert self.qoff.shape == (Z, Y, X, 6)
+        self.sc.qoff = self.qoff.ctypes.data
+        self.sc.chunk = chunk
+        self.sc.unit_split = 1 if quad is False or quad is None else 0
 
     def hold_exit_table(self, params):
         """Build the exit table the frame `params` reads (exit mode, every sample

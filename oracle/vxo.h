@@ -52,6 +52,8 @@ typedef struct {
                                  primary records then carry v_cellPos = the quad origin and v_fractPos = the hit
                                  point minus it, as render.vert:25-28 hands them over.  NULL: the unit cell. */
     int chunk;                /* the mesher's CHUNK (voxmap.h:9: Z); <= 0 -> Z */
+    int unit_split;           /* 1: the unit-cell split even with qoff set (qoff then serves the glass draw
+                                 order only); a frame's flag VXO_FLAG_UNIT_GBUF does the same per frame */
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */
@@ -83,6 +85,8 @@ typedef struct {
  * the single layer.  Needs the quad table (vxo_scene.qoff).  Up to
  * VXO_MAX_GLASS glass faces per pixel (the nearest ones) are blended. */
 #define VXO_FLAG_GLASS_ORDER 0x1000u
+#define VXO_FLAG_UNIT_GBUF 0x800u   /* the unit-cell G-buffer split (include/voxmap.h VX_FLAG_UNIT_GBUF) */
+#define VXO_FLAG_REFLECT_ALL 0x2000u /* ext: the first surface of every pixel mirrors the scene (as REFLECT glass) */
 #define VXO_MAX_GLASS 8
 
 typedef struct {

@@ -445,7 +445,8 @@ static int primary_walk(const vxo_scene *s, const vxo_frame *f, const float d[3]
         int lo = -cc[i], hi = dims[i] - cc[i] - 1;
         c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
     }
-    return walk(s, cc, o, d, c, glass_layer, g, fetches, cap_hit, NULL, 1);
+    const int quad = !s->unit_split && !(f->flags & VXO_FLAG_UNIT_GBUF);
+    return walk(s, cc, o, d, c, glass_layer, g, fetches, cap_hit, NULL, quad);
 }
 
 int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
@@ -844,6 +845,17 @@ static void reflect_color(const shade_ctx *c, const vxo_gbuf *gl, const float rd
     out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
 }
 
+/* ext REFLECT / REFLECT_ALL: rgb += F * the colour along the mirror ray, Schlick's
+ * Fresnel with F0 = 0.04 on the geometric normal (cos = |rayDir| along the face axis) */
+static void add_reflection(const shade_ctx *c, const vxo_gbuf *g, const float rd[3], float rgb[3], vxo_stats *st) {
+    float refl[3];
+    reflect_color(c, g, rd, refl, st);
+    const float cs = g_min(fabsf(rd[g->normal_idx >> 1]), 1.0f);
+    const float x = 1.0f - cs, x2 = x * x;
+    const float F = 0.04f + 0.96f * ((x2 * x2) * x);
+    for (int i = 0; i < 3; i++) rgb[i] = rgb[i] + F * refl[i];
+}
+
 /* 2D mode (u_quality = 0): drawScene binds the vertex2d mesh (render.js:278,
  * 287): the footprint quads of sdf.cpp:362-401 on the plane z = 0, vert2d
  * normal byte 0 -> v_normal = (1,0,0) (render.vert:16), culled from below
@@ -965,14 +977,7 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
             g_term_slot = idx[k] == 0 ? 0 : -1;
             shade_frag(c, gl, NULL, src, rd, st);
             g_term_slot = -1;
-            if (f->flags & VXO_FLAG_REFLECT) {
-                float refl[3];
-                reflect_color(c, gl, rd, refl, st);
-                const float cs = g_min(fabsf(rd[gl->normal_idx >> 1]), 1.0f);
-                const float x = 1.0f - cs, x2 = x * x;
-                const float F = 0.04f + 0.96f * ((x2 * x2) * x);
-                for (int i = 0; i < 3; i++) src[i] = src[i] + F * refl[i];
-            }
+            if (f->flags & (VXO_FLAG_REFLECT | VXO_FLAG_REFLECT_ALL)) add_reflection(c, gl, rd, src, st);
             const float a = src[3];
             for (int i = 0; i < 3; i++) dst[i] = src[i] * a + dst[i] * (1.0f - a);
             depth = gl->t;
@@ -981,24 +986,17 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
     } else if (g[0].id != 2) {
         if (st) st->block_px++;
         g_term_slot = 0;
-        shade_frag(c, &g[0], NULL, out, NULL, st);
+        float rd[3];
+        shade_frag(c, &g[0], NULL, out, rd, st);
         g_term_slot = -1;
+        if (f->flags & VXO_FLAG_REFLECT_ALL) add_reflection(c, &g[0], rd, out, st);
     } else {
         if (st) st->glass_px++;
         float src[4], dst[4], rd[3];
         g_term_slot = 0;
         shade_frag(c, &g[0], NULL, src, rd, st);
         g_term_slot = -1;
-        if (f->flags & VXO_FLAG_REFLECT) {
-            /* Schlick's Fresnel with F0 = 0.04 on the geometric normal:
-             * cos = |rayDir| along the face axis */
-            float refl[3];
-            reflect_color(c, &g[0], rd, refl, st);
-            const float cs = g_min(fabsf(rd[g[0].normal_idx >> 1]), 1.0f);
-            const float x = 1.0f - cs, x2 = x * x;
-            const float F = 0.04f + 0.96f * ((x2 * x2) * x);
-            for (int i = 0; i < 3; i++) src[i] = src[i] + F * refl[i];
-        }
+        if (f->flags & (VXO_FLAG_REFLECT | VXO_FLAG_REFLECT_ALL)) add_reflection(c, &g[0], rd, src, st);
         g_term_slot = 1;
         if (n == 2) shade_frag(c, &g[1], NULL, dst, NULL, st);
         else shade_frag(c, &sky, d, dst, NULL, st);

@@ -243,3 +243,23 @@ def test_scene_generators_deterministic():
     c = scenes.s_campus()
     assert c.shape == (32, 256, 1024) and (c[0] > 0).all() and c[1:].any()
     assert scenes.upsample3(scenes.single_block()).shape == (48, 96, 192)
+
+
+def test_offset_limits_rejected_before_any_upload(built):
+    """the AO pair array (4 B per cell, X + 1 per row) and the noise
+    quad planes (16 B per texel) use 32-bit byte offsets; fields and noise past
+    them are refused by vx_scene_create's checks (no GPU touched)."""
+    import voxmap_amd as vx
+    with pytest.raises(vx.VoxmapError) as e:
+        vx.Scene(map_bytes=b"\x00" * 64, map_format=vx.FORMAT_BIN, dims=(2048, 2100, 250))
+    assert e.value.code == -1 and "4*(X+1)*Y*Z" in str(e.value)
+    # just below the limit the same check passes (then the 64-byte map is the wrong size)
+    with pytest.raises(vx.VoxmapError) as e:
+        vx.Scene(map_bytes=b"\x00" * 64, map_format=vx.FORMAT_BIN, dims=(2048, 2040, 250))
+    assert e.value.code == -5
+    with pytest.raises(vx.VoxmapError) as e:
+        vx.Scene(map_bytes=b"\x00" * 256, map_format=vx.FORMAT_BIN, dims=(4, 4, 4), noise_size=(16384, 16384))
+    assert e.value.code == -1 and "noise too large" in str(e.value)
+    with pytest.raises(vx.VoxmapError) as e:
+        vx.Scene(map_bytes=b"\x00" * 256, map_format=vx.FORMAT_BIN, dims=(4, 4, 4), mesh_chunk=300)
+    assert e.value.code == -1 and "mesh_chunk" in str(e.value)

@@ -146,3 +146,82 @@ def test_mesh_chunk_option(noise):
     ref, ost = oracle.Oracle(field, noise, exit=True, quad=ref_q, chunk=16).render(fr.params, 200, 120)
     _compare(img, ref)
     _counters_equal(st, ost)
+
+
+GLASS_CASES = [
+    # small S-glass scenes: hollow pavilions and screens, cameras toward -x/-y
+    # (far panes' quads drawn first: both blend) and +x
+    (2, (96, 64, 16), (48.0, 32.0, 20.0), (1.1, 0.0, 0.6)),
+    (3, (96, 64, 16), (48.0, 32.0, 20.0), (1.2, 0.0, 2.6)),
+    (4, (128, 64, 24), (64.0, 32.0, 14.0), (1.3, 0.0, -2.2)),
+]
+
+
+@pytest.mark.parametrize("seed,dims,sbj,rot", GLASS_CASES)
+@pytest.mark.parametrize("flags,samples", [(0x1000, 0), (48 | 0x1000, 0), (0x2000 | 0x1000 | 32, 0),
+                                           (48 | 0x1000, 16), (48 | 0x1000 | 0x80, 16)],
+                         ids=["order_v1", "order_full", "order_reflect_all", "order_soft16", "order_soft16_pool"])
+def test_glass_order_small(noise, seed, dims, sbj, rot, flags, samples):
+    """Glass in draw order (VX_FLAG_GLASS_ORDER, render.js:82-91) against the
+    oracle's restatement, every pixel and counter; the frame differs from the
+    single layer on the pixels whose ray crosses two or more panes."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    field = vx.field_build(scenes.s_glass(seed, dims=dims, n_houses=12, n_facades=4))
+    fr = vx.make_frame(sbj, rot, 200, 120, flags=flags, shadow_samples=samples, sun_radius=0.04)
+    with _scene(vx, field, noise, dims) as sc:
+        img, st = sc.render(fr, stats=True)
+    O = oracle.Oracle(field, noise, exit=True)
+    ref, ost = O.render(fr.params, 200, 120)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+    assert st.glass_px > 500
+
+
+@pytest.mark.parametrize("cam", ["K1", "K2"])
+def test_s_glass_c3_draw_order(noise, cam):
+    """S-glass C3 full quality with glass in draw order: every pixel against the
+    oracle, and (K1) the pixels that change against the single layer."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_glass"))
+    fr = presets.camera_frame(cam, 3840, 2160, flags=vx.FLAG_FULL_QUALITY | vx.FLAG_GLASS_ORDER)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 3840, 2160, threads=16)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+
+
+@pytest.mark.parametrize("seed,dims,sbj,rot", SMALL)
+@pytest.mark.parametrize("flags", [0x2000, 0x2000 | 32, 0x2000 | 48], ids=["reflect_all", "reflect_all_rough", "full_all"])
+def test_reflect_all_small(noise, seed, dims, sbj, rot, flags):
+    """VX_FLAG_REFLECT_ALL: every first surface mirrors the traced scene."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    field = vx.field_build(scenes.small_proc(seed, dims=dims, n_boxes=16, n_glass=6))
+    fr = vx.make_frame(sbj, rot, 160, 96, flags=flags)
+    with _scene(vx, field, noise, dims) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 160, 96)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+    assert st.reflect_rays >= st.block_px
+
+
+def test_reflect_all_c3(noise):
+    """The bench's c3_reflect_all frame (full quality + REFLECT_ALL) at C3."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_proc"))
+    fr = presets.camera_frame("K1", 3840, 2160, flags=vx.FLAG_FULL_QUALITY | vx.FLAG_REFLECT_ALL)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 3840, 2160, threads=16)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+    assert st.reflect_rays > 6_000_000

@@ -81,6 +81,7 @@ class Stats(C.Structure):
         ("ao_samples", C.c_uint64), ("noise_px", C.c_uint64), ("primary_cap_hits", C.c_uint64),
         ("reflect_rays", C.c_uint64), ("reflect_fetches", C.c_uint64), ("rough_px", C.c_uint64),
         ("primary_wave_iters", C.c_uint64), ("march_wave_iters", C.c_uint64), ("march_lane_slots", C.c_uint64),
+        ("shadow_rays_resolved", C.c_uint64),
         ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double),
     ]
 

@@ -38,6 +38,10 @@ struct vx_scene {
         int8_t *d = nullptr;
         hipEvent_t ready = nullptr;
         unsigned long long used = 0;
+        // one event per stream that enqueued a render reading this copy since it
+        // was built (recorded after the launch, under cone_mu): recycling the slot
+        // waits for exactly those readers
+        std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
     } cones[2];
     unsigned long long cone_tick = 0;
     std::mutex cone_mu;
@@ -199,10 +203,19 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
 #endif
             // per ray octant, the channel with every cell whose orthant ahead holds no block
             // marked -1: the march exits "lit" there (DESIGN.md §3 "Orthant exit")
-            if (VX_SUNX && !lrc && e == hipSuccess && (e = hipMalloc(&s->d_sunx, 8 * np)) == hipSuccess &&
-                (e = hipMemsetAsync(s->d_sunx, 0xFF, 8 * np, s->stream)) == hipSuccess)
-                lrc = launch_sun_exit(s->d_sunp, s->d_sunx, ga, X, Y, Z, s->SB, s->stream);
             if (e != hipSuccess) lrc = (int)e;
+            // the exit tables are an optimisation (the kernel marches the plain
+            // channel when a.sunx is null): a copy that does not fit leaves them off
+            if (VX_SUNX && !lrc) {
+                if (hipMalloc(&s->d_sunx, 8 * np) != hipSuccess) {
+                    (void)hipGetLastError();
+                    s->d_sunx = nullptr;
+                } else if ((e = hipMemsetAsync(s->d_sunx, 0xFF, 8 * np, s->stream)) == hipSuccess) {
+                    lrc = launch_sun_exit(s->d_sunp, s->d_sunx, ga, X, Y, Z, s->SB, s->stream);
+                } else {
+                    lrc = (int)e;
+                }
+            }
         }
         for (int oct = 0; oct < 8 && !lrc; oct++) {
             lrc = launch_field_octant(lin, X, Y, Z, cap, oct, ga, gb, s->stream);
@@ -234,6 +247,7 @@ void vx_scene_destroy(vx_scene *s) {
     for (auto &c : s->cones) {
         if (c.d) (void)hipFree(c.d);
         if (c.ready) (void)hipEventDestroy(c.ready);
+        for (auto &r : c.readers) (void)hipEventDestroy(r.second);
     }
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_rg2) (void)hipFree(s->d_rg2);
@@ -323,6 +337,7 @@ static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int 
     st->primary_wave_iters = v[ST_PRIM_WITERS];
     st->march_wave_iters = v[ST_MARCH_WITERS];
     st->march_lane_slots = v[ST_MARCH_SLOTS];
+    st->shadow_rays_resolved = v[ST_SHADOW_RESOLVED];
     // 4 B per field texel read (primary, shadow and reflection
     // rays), 32 B per trilinear AO, 80 B per clouded sky pixel (5 bilinear
     // noise taps), 16 B per rough-normal white() tap (4 texels), plus the
@@ -344,11 +359,14 @@ struct TileSpec {
 
 // The frame's cone copy {oct, kx, ky}: found in the scene's cache (the
 // stream waits for its build), or built on stream st into a free or the least
-// recently used slot -- after a device-wide synchronise when that slot's copy
-// may still be read by a frame in flight.
-static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built) {
+// recently used slot -- after every render enqueued so far that reads that
+// slot has finished (its readers' events).  The caller holds s->cone_mu from
+// here until its render is enqueued and recorded as a reader (note_reader), so
+// no other thread can recycle the slot in between.  t_build: recorded on st
+// just before the build's first packet (vx_prepare_sun's timing), if built.
+static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built,
+                     vx_scene::Cone **used, hipEvent_t t_build) {
     *built = false;
-    std::lock_guard<std::mutex> lock(s->cone_mu);
     vx_scene::Cone *slot = nullptr;
     for (auto &c : s->cones)
         if (c.d && c.oct == oct && c.kx == kx && c.ky == ky) slot = &c;
@@ -357,13 +375,14 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         for (auto &c : s->cones)
             if (!c.d || c.used < slot->used) slot = &c;
         if (slot->d) {
-            VX_HIP(hipDeviceSynchronize());
+            for (auto &r : slot->readers) VX_HIP(hipEventSynchronize(r.second));
         } else {
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
             VX_HIP(hipMalloc(&slot->d, np));
             if (!slot->ready) VX_HIP(hipEventCreateWithFlags(&slot->ready, hipEventDisableTiming));
         }
         slot->oct = -1;
+        if (t_build) VX_HIP(hipEventRecord(t_build, st));
         VX_HIP(hipMemsetAsync(slot->d, 0xFF, (size_t)s->SXp * s->SYp * s->SZp, st));
         const int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
         if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
@@ -375,21 +394,38 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
     }
     slot->used = ++s->cone_tick;
     *out = slot->d;
+    *used = slot;
+    return VX_OK;
+}
+
+// After a render reading cone copy c was enqueued on st (cone_mu held): record it as a reader.
+static int note_reader(vx_scene::Cone *c, hipStream_t st) {
+    for (auto &r : c->readers)
+        if (r.first == st) {
+            VX_HIP(hipEventRecord(r.second, st));
+            return VX_OK;
+        }
+    hipEvent_t e = nullptr;
+    VX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->readers.emplace_back(st, e);
+    VX_HIP(hipEventRecord(e, st));
     return VX_OK;
 }
 
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
 // a.sunc (cone) built or found, and the info filled
 static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &fc, hipStream_t st,
-                      const int8_t **sunc, vx_exit_info *info, bool *built = nullptr) {
+                      const int8_t **sunc, vx_exit_info *info, bool *built, vx_scene::Cone **used,
+                      hipEvent_t t_build = nullptr) {
     *sunc = nullptr;
+    *used = nullptr;
     bool b = false;
     vx_exit_info e{0, -1, -1, -1, 0.0f};
     const bool tables = s->d_sunx && !(p->flags & VX_FLAG_NO_EXIT);
     if (tables && p->quality != 0 && !(p->flags & (VX_FLAG_NO_SHADOW | VX_FLAG_PRIMARY_ONLY))) {
         int oct, kx, ky;
         if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
-            const int rc = cone_copy(s, oct, kx, ky, st, sunc, &b);
+            const int rc = cone_copy(s, oct, kx, ky, st, sunc, &b, used, t_build);
             if (rc) return rc;
             e = vx_exit_info{2, oct, kx, ky, 0.0f};
         } else if (fc.sun_k[0].fast) {
@@ -422,6 +458,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.fp2d = s->d_fp2d;
     a.qface = s->d_qface;
     a.quad_gbuf = (p->flags & VX_FLAG_UNIT_GBUF) ? 0 : 1;
+    a.chunk = s->chunk;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;
     a.noise_w = s->noise_w; a.noise_h = s->noise_h;
     a.noise_rw = 1.0f / (float)s->noise_w;   // powers of two: exact
@@ -440,10 +477,16 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.p = *p;
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
+    // the cone copy the frame reads stays pinned from its lookup until this
+    // render is enqueued and recorded as its reader (a second thread
+    // must not recycle it in between)
+    std::unique_lock<std::mutex> cone_lock(s->cone_mu);
+    vx_scene::Cone *cone = nullptr;
     {
-        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr);
+        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
         if (rc) return rc;
     }
+    if (!cone) cone_lock.unlock();
     a.Xp = s->L.Xp;
     a.pad = s->L.pad;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
@@ -476,6 +519,11 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     if (stats) VX_HIP(hipEventRecord(s->ev0, st));
     int rc = launch_render(a, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("render launch failed: ") + hipGetErrorString((hipError_t)rc));
+    if (cone) {
+        rc = note_reader(cone, st);
+        cone_lock.unlock();
+        if (rc) return rc;
+    }
     if (stats) VX_HIP(hipEventRecord(s->ev1, st));
     if (stats) {
         unsigned long long v[ST_COUNT];
@@ -499,10 +547,15 @@ int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_
     frame_consts(*p, 64, 64, s->X, s->Y, s->Z, max_steps, fc);
     const int8_t *sunc = nullptr;
     bool built = false;
-    VX_HIP(hipEventRecord(s->ev0, st));
-    rc = frame_exit(s, p, fc, st, &sunc, info, &built);
-    if (rc) return rc;
-    VX_HIP(hipEventRecord(s->ev1, st));
+    vx_scene::Cone *cone = nullptr;
+    {
+        // ev0 is recorded inside cone_copy right before the build's first packet:
+        // build_ms is the copy's GPU time, not the host's allocation or waits
+        std::lock_guard<std::mutex> lock(s->cone_mu);
+        rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, s->ev0);
+        if (rc) return rc;
+        if (built) VX_HIP(hipEventRecord(s->ev1, st));
+    }
     VX_HIP(hipStreamSynchronize(st));
     if (info && built) {
         float ms = 0.0f;

@@ -86,6 +86,7 @@ struct KernelArgs {
     const uint32_t *fp2d;    // 2D mode: 2 words per column (x fastest): vis colour, quad corner x0 | y0 << 16
     const uint16_t *qface;   // greedy mesh per face: plane n (normal index) of X*Y*Z u16, du | dv << 8 (launch_face_quads)
     int quad_gbuf;           // 1: fragments carry the quad-relative split (render.vert:25-28); 0: the unit cell
+    int chunk;               // the mesh's CHUNK (glass draw order, face_key)
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
     float noise_rw, noise_rh;    // 1/noise_w, 1/noise_h (exact)
@@ -124,7 +125,7 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
 enum StatSlot {
     ST_PIXELS = 0, ST_SKY, ST_BLOCK, ST_GLASS, ST_PRIM_FETCH, ST_SHADOW_RAYS, ST_SHADOW_FETCH,
     ST_AO, ST_NOISE_PX, ST_CAP_HITS, ST_REFL_RAYS, ST_REFL_FETCH, ST_ROUGH, ST_PRIM_WITERS, ST_MARCH_WITERS,
-    ST_MARCH_SLOTS, ST_COUNT
+    ST_MARCH_SLOTS, ST_SHADOW_RESOLVED, ST_COUNT
 };
 
 // Field data in HBM (vx_kernels.hip): `prim` = 8 copies (one

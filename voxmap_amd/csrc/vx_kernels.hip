@@ -149,6 +149,7 @@ struct Counters {
     unsigned refl_rays, refl_fetch, rough;   // extensions
     unsigned prim_witers, march_witers;      // loop iterations per wave (diagnostic: lane utilisation)
     unsigned march_slots;                    // per march wave iteration: the lanes that began that march
+    unsigned shadow_resolved;                // shadow rays resolved by the first-step table test (not marched)
 };
 
 // (float)((t >> 8k) & 0xff) as one v_cvt_f32_ubyteK (left to itself the
@@ -670,7 +671,7 @@ __device__ __forceinline__ void quad_offsets(const KernelArgs &a, int ax, int ni
 // [c, c + E*s] lies ahead of the ray: h and A bracket it on every axis.
 template <bool F32IDX>
 __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d2, Surf &g0, Surf &g1,
-                       Counters &cnt) {
+                       Counters &cnt, float &t_hit) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
     const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
@@ -842,7 +843,146 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         h.f2 = hax == 2 ? 0.0f : (o2 + te * d2) - r2;
         nrec++;
     }
+    t_hit = te;
     return nrec;
+}
+
+// ---------------- glass in draw order (VX_FLAG_GLASS_ORDER) ----------------
+// The reference draws the glass quads after every opaque one, in vertex.bin
+// order, with depth test LESS and depth writes on, blending SRC_ALPHA
+// (render.js:82-91, sdf.cpp:284,337).  face_key is that order for a glass
+// face (oracle vxo_face_order): forChunkXYZ chunk, axis d, normal, slice, quad
+// origin row j, column i; a face on an interior chunk plane is emitted first
+// by the lower chunk (its slice CH-1).
+__device__ __forceinline__ unsigned long long face_key(const KernelArgs &a, int x, int y, int z, int nidx,
+                                                       unsigned q) {
+    const int CH = a.chunk;
+    const int d = nidx >> 1, normal = nidx & 1;
+    const int cd_ = d == 0 ? x : (d == 1 ? y : z);                  // cell along d, u, v
+    const int cu = d == 0 ? y : (d == 1 ? z : x);
+    const int cv = d == 0 ? z : (d == 1 ? x : y);
+    const int plane = cd_ + (normal ? 0 : 1);
+    int kd = plane / CH, pd = plane % CH - 1;
+    if (pd < 0) { kd -= 1; pd = CH - 1; }
+    const int ou = cu - (int)(q & 0xffu), ov = cv - (int)(q >> 8);
+    const int ku = ou / CH, kv = ov / CH;
+    const int kx = d == 0 ? kd : (d == 1 ? kv : ku);
+    const int ky = d == 1 ? kd : (d == 2 ? kv : ku);
+    const int kz = d == 2 ? kd : (d == 0 ? kv : ku);
+    const unsigned long long ny = (unsigned long long)((a.Y + CH - 1) / CH), nz = (unsigned long long)((a.Z + CH - 1) / CH);
+    const unsigned long long S = (unsigned long long)CH + 1;
+    const unsigned long long chunk = ((unsigned long long)kx * ny + (unsigned long long)ky) * nz + (unsigned long long)kz;
+    return ((((chunk * 3 + (unsigned long long)d) * 2 + (unsigned long long)normal) * S + (unsigned long long)(pd + 1)) * S +
+            (unsigned long long)(ov - kv * CH)) * S + (unsigned long long)(ou - ku * CH);
+}
+
+// One pass over the view ray's glass faces (the walk of primary visibility,
+// scalar form like walk_reflect; oracle walk() with glass_layer 2): of the
+// nearest VX_MAX_GLASS_LAYERS front-facing glass entries before the first
+// opaque entry, the one drawn first after key `klast` (none: have_last false)
+// among those nearer than tmax.  Returns false if there is none; else its
+// G-buffer record (quad-relative unless a.quad_gbuf is 0), depth and key.
+// Its fetches repeat the primary walk's and are not counted again.
+__device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float d1, float d2, bool have_last,
+                                           unsigned long long klast, float tmax, Surf &h, float &t_out,
+                                           unsigned long long &k_out) {
+    const FrameConsts &F = a.fc;
+    const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
+    const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
+    const float iv0 = d0 != 0.0f ? 1.0f / d0 : 0.0f, iv1 = d1 != 0.0f ? 1.0f / d1 : 0.0f,
+                iv2 = d2 != 0.0f ? 1.0f / d2 : 0.0f;
+    float tlo = 0.0f, thi = kInf;
+    bool miss = false;
+    auto slab = [&](float d, float iv, int i) {
+        const float lo = F.slab_lo[i], hi = F.slab_hi[i];
+        if (d != 0.0f) {
+            float t0 = lo * iv, t1 = hi * iv;
+            if (t0 > t1) { const float tt = t0; t0 = t1; t1 = tt; }
+            tlo = gmax(tlo, t0);
+            thi = gmin(thi, t1);
+        } else if (!(lo <= 0.0f && 0.0f < hi)) {
+            miss = true;
+        }
+    };
+    slab(d0, iv0, 0); slab(d1, iv1, 1); slab(d2, iv2, 2);
+    if (miss || !(tlo < thi)) return false;
+    auto entry = [&](float o, float d, int cc, int dim) {
+        const int c = f2i(floorf(o + tlo * d));
+        return min(max(c, -cc), dim - cc - 1);
+    };
+    int c0 = entry(o0, d0, cc0, a.X), c1 = entry(o1, d1, cc1, a.Y), c2 = entry(o2, d2, cc2, a.Z);
+    const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
+    const uint32_t *pp = a.prim + (size_t)oct * a.copy_texels;
+    auto fetch = [&](int x, int y, int z) -> uint32_t {
+        return pp[(unsigned)(x + a.pad) + (unsigned)a.Xp * (unsigned)(y + a.pad) + a.XpYp * (unsigned)(z + a.pad)];
+    };
+    const int st0 = d0 > 0.0f ? 1 : -1, st1 = d1 > 0.0f ? 1 : -1, st2 = d2 > 0.0f ? 1 : -1;
+    uint32_t t = fetch(c0 + cc0, c1 + cc1, c2 + cc2);
+    int prev = t & 0xff, e0 = (int)((t >> 8) & 0xff), e1 = (int)((t >> 16) & 0xff), e2 = (int)(t >> 24);
+    bool found = false;
+    int nglass = 0, bx = 0, by = 0, bz = 0, bax = 0, bst = 0;
+    unsigned bq = 0;
+    float bt = 0.0f;
+    unsigned long long bk = 0;
+    const int cap = 4 * (a.X + a.Y + a.Z);
+    for (int it = 0; it < cap; it++) {
+        const float tb0 = d0 != 0.0f ? ((float)(c0 + (st0 > 0 ? e0 + 1 : -e0)) - o0) * iv0 : kInf;
+        const float tb1 = d1 != 0.0f ? ((float)(c1 + (st1 > 0 ? e1 + 1 : -e1)) - o1) * iv1 : kInf;
+        const float tb2 = d2 != 0.0f ? ((float)(c2 + (st2 > 0 ? e2 + 1 : -e2)) - o2) * iv2 : kInf;
+        const int ax = (tb0 <= tb1 && tb0 <= tb2) ? 0 : (tb1 <= tb2 ? 1 : 2);
+        const float te = ax == 0 ? tb0 : (ax == 1 ? tb1 : tb2);
+        auto side = [&](int c, float o, float d, int e) {
+            const int v = f2i(floorf(o + te * d));
+            const int lo = d < 0.0f ? c - e : c, hi = d < 0.0f ? c : c + e;
+            return v < lo ? lo : (v > hi ? hi : v);
+        };
+        const int n0 = ax == 0 ? c0 + st0 * (e0 + 1) : side(c0, o0, d0, e0);
+        const int n1 = ax == 1 ? c1 + st1 * (e1 + 1) : side(c1, o1, d1, e1);
+        const int n2 = ax == 2 ? c2 + st2 * (e2 + 1) : side(c2, o2, d2, e2);
+        c0 = n0; c1 = n1; c2 = n2;
+        const int x = c0 + cc0, y = c1 + cc1, z = c2 + cc2;
+        if ((unsigned)x >= (unsigned)a.X || (unsigned)y >= (unsigned)a.Y || (unsigned)z >= (unsigned)a.Z) break;
+        t = fetch(x, y, z);
+        const int col = t & 0xff;
+        e0 = (int)((t >> 8) & 0xff); e1 = (int)((t >> 16) & 0xff); e2 = (int)(t >> 24);
+        if (col != prev && col != 0) {             // a front face
+            if (col != kGlass) break;              // the opaque surface: no glass behind it is drawn
+            if (nglass < VX_MAX_GLASS_LAYERS) {
+                nglass++;
+                const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
+                const int nidx = 2 * ax + (stp > 0 ? 1 : 0);
+                unsigned q = a.qface[(size_t)nidx * a.XYZ + lin_index(a, x, y, z)];
+                q = q == 0xFFFFu ? 0u : q;
+                const unsigned long long k = face_key(a, x, y, z, nidx, q);
+                if ((!have_last || k > klast) && te < tmax && (!found || k < bk)) {
+                    found = true;
+                    bk = k; bt = te; bq = q; bax = ax; bst = stp;
+                    bx = c0; by = c1; bz = c2;
+                }
+            }
+        }
+        prev = col;
+    }
+    if (!found) return false;
+    // the record (primary()'s rule): face axis on its plane, the others quad-relative
+    unsigned q = a.quad_gbuf ? bq : 0u;
+    const int lo = (int)(q & 0xffu), hi = (int)(q >> 8);
+    const int of0 = bax == 2 ? lo : (bax == 1 ? hi : 0);
+    const int of1 = bax == 0 ? lo : (bax == 2 ? hi : 0);
+    const int of2 = bax == 1 ? lo : (bax == 0 ? hi : 0);
+    const int up = bst > 0 ? 0 : 1;
+    h.id = 2;
+    h.color = kGlass;
+    h.nidx = 2 * bax + (bst > 0 ? 1 : 0);
+    h.c0 = bx - of0 + cc0 + (bax == 0 ? up : 0);
+    h.c1 = by - of1 + cc1 + (bax == 1 ? up : 0);
+    h.c2 = bz - of2 + cc2 + (bax == 2 ? up : 0);
+    h.f0 = bax == 0 ? 0.0f : (o0 + bt * d0) - (float)(bx - of0);
+    h.f1 = bax == 1 ? 0.0f : (o1 + bt * d1) - (float)(by - of1);
+    h.f2 = bax == 2 ? 0.0f : (o2 + bt * d2) - (float)(bz - of2);
+    t_out = bt;
+    k_out = bk;
+    return true;
 }
 
 // ---------------- sampling ----------------
@@ -1111,6 +1251,7 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
             shadeFactor = shadeFactor * ((float)lit_given / (float)F.n_sun);
         } else if (first_exit) {       // every sample's first step lands in the marked block
             cnt.shadow_rays += (unsigned)F.n_sun;
+            cnt.shadow_resolved += (unsigned)F.n_sun;
         } else {                       // ext soft shadows (EXT == 2): lit fraction of the sun samples
             int lit = 0;
             if (xch) {                 // one sign pattern, one copy: the shared-start loop
@@ -1447,7 +1588,10 @@ void k_render(KernelArgs a) {
         // the field copy of this ray's octant (zero components count positive)
         const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
         Surf g[2];
-        const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt);
+        float t_hit;
+        const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt, t_hit);
+        // glass in draw order (EXT >= 1 only; launch_render routes such v1 frames to EXT 1)
+        const bool order = XE >= 1 && (F.flags & VX_FLAG_GLASS_ORDER);
         int lit0 = -1;
         if (kPool && !inframe) cnt = Counters{};
         if (kPool && F.soft_sg >= 0 && a.sunp) {
@@ -1458,8 +1602,9 @@ void k_render(KernelArgs a) {
             // surface points instead of one line per pixel, and lanes whose own
             // pixel does not march (sky, faces turned from the sun) march for
             // the others.  Same exact march_pad, lit counted per fragment in LDS.
+            // (a glass pixel in draw order may shade other panes first: it marches in shade_block)
             const bool need = inframe && n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
-                              block_shade_factor<XE>(a, g[0]) > 0.0f;
+                              !(order && g[0].id == 2) && block_shade_factor<XE>(a, g[0]) > 0.0f;
             const unsigned long long mask = __ballot(need);
             if (mask) {
                 const int wb = threadIdx.x & ~63;                // this wave's 64 slots
@@ -1564,28 +1709,49 @@ void k_render(KernelArgs a) {
                 // 64-VGPR budget).  Shading has no side effects besides the
                 // counters (sums), so the order changes no result.
                 float dst[4];
-                if (g[0].id == 2) {
+                const bool glass = g[0].id == 2;
+                if (glass) {
                     if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
                     else shade_sky(a, d0, d1, d2, dst, cnt);
                 }
-                float rd[3];
-                shade_block<XE>(a, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
-                if (g[0].id == 2) {
-                    n_glass = 1;
-                    if (XE && (F.flags & VX_FLAG_REFLECT)) {
+                // The first surface; for glass, the panes blended over what is
+                // behind: the nearest one (single layer), or in draw order each
+                // pane nearer than the last one written (order: glass_scan finds
+                // the next, render.js:82-91).  One shade_block site for all of them.
+                Surf cur = g[0];
+                float depth = n == 2 ? t_hit : kInf;
+                unsigned long long klast = 0;
+                bool have_last = false;
+                for (;;) {
+                    if (order && glass) {
+                        float tc;
+                        unsigned long long kc;
+                        if (!glass_scan(a, d0, d1, d2, have_last, klast, depth, cur, tc, kc)) break;
+                        depth = tc; klast = kc; have_last = true;
+                    }
+                    float rd[3];
+                    shade_block<XE>(a, cur, rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, order && glass ? -1 : lit0);
+                    // ext REFLECT (glass panes) / REFLECT_ALL (every first surface and pane)
+                    if (XE && (F.flags & (glass ? (VX_FLAG_REFLECT | VX_FLAG_REFLECT_ALL) : VX_FLAG_REFLECT_ALL))) {
                         // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
                         float refl[3];
-                        reflect_color<XE>(a, g[0], rd, refl, cnt);
-                        const int ax = g[0].nidx >> 1;
+                        reflect_color<XE>(a, cur, rd, refl, cnt);
+                        const int ax = cur.nidx >> 1;
                         const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
                         const float x = 1.0f - cs, x2 = x * x;
                         const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
 #pragma unroll
                         for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
                     }
+                    if (!glass) break;
                     const float al = rgba[3];
 #pragma unroll
-                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+                    for (int i = 0; i < 3; i++) dst[i] = rgba[i] * al + dst[i] * (1.0f - al);
+                    if (!order) break;
+                }
+                if (glass) {
+                    n_glass = 1;
+                    rgba[0] = dst[0]; rgba[1] = dst[1]; rgba[2] = dst[2];
                 } else {
                     n_block = 1;
                 }
@@ -1625,6 +1791,7 @@ void k_render(KernelArgs a) {
         v[ST_PRIM_WITERS] = wave_sum(cnt.prim_witers);
         v[ST_MARCH_WITERS] = wave_sum(cnt.march_witers);
         v[ST_MARCH_SLOTS] = wave_sum(cnt.march_slots);
+        v[ST_SHADOW_RESOLVED] = wave_sum(cnt.shadow_resolved);
         if (lane == 0) {
             // spread the adds over 64 slot rows to avoid one hot line per counter
             unsigned long long *row = a.stats + (size_t)((blockIdx.x + blockIdx.y * 7) & 63) * ST_COUNT;
@@ -1781,7 +1948,8 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
     const bool brick_ok = a.fc.soft_sg >= 0 && a.sunp && a.fc.soft_lg >= 4 && (a.SXp & 3) == 0 && a.SB >= 9;
     const int ext = a.fc.n_sun > 1 ? ((a.fc.flags & VX_FLAG_SOFT_BRICK) && brick_ok ? 4
                                       : (a.fc.flags & (VX_FLAG_SOFT_POOL | VX_FLAG_SOFT_BRICK)) ? 3 : 2)
-                                   : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
+                                   : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH | VX_FLAG_GLASS_ORDER |
+                                                     VX_FLAG_REFLECT_ALL)) ? 1 : 0);
 #define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
 #define VX_LE(F, S, T) do { if (ext == 4) VX_L(F, S, T, 4); else if (ext == 3) VX_L(F, S, T, 3); \
                                 else if (ext == 2) VX_L(F, S, T, 2); \
