@@ -164,3 +164,25 @@ def test_two_threads_cycle_three_suns(scene):
     for t in ts:
         t.join()
     assert not errors, errors[:5]
+
+
+@pytest.mark.parametrize("flags", [48], ids=["full"])
+def test_c3_full_size_no_exit_equals_exit_tables(noise, flags):
+    """VERDICT r03 housekeeping: the bench's C3 K1 frame (3840x2160, full
+    quality) marched without the exit tables (VX_FLAG_NO_EXIT: every step of
+    render.frag:92-136) equals the exit-table frame bit for bit, and its shadow
+    fetch count is the oracle's literal march's."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_proc"))
+    with vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=(1024, 256, 32), device=0) as sc:
+        fr = presets.camera_frame("K1", 3840, 2160, flags=flags)
+        a, sa = sc.render(fr, stats=True)
+        fn = presets.camera_frame("K1", 3840, 2160, flags=flags | vx.FLAG_NO_EXIT)
+        b, sb = sc.render(fn, stats=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sb.shadow_fetches > 3 * sa.shadow_fetches
+    _, ost = oracle.Oracle(field, noise).render(fn.params, 3840, 2160, row0=0, row_step=1, threads=16)
+    assert sb.shadow_fetches == ost.shadow_fetches and sb.primary_fetches == ost.primary_fetches

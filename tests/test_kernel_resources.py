@@ -17,8 +17,9 @@ def _render(meta):
 
 
 def test_every_render_instantiation_present(meta):
-    # FMT 2 x STATS 2 x TILED 2 x EXT mode 5 (v1, ext, soft, soft pooled, soft LDS bricks) x primary index 2
-    assert len(_render(meta)) == 80
+    # FMT 2 x STATS 2 x TILED 2 x (EXT modes 0-4 (v1, ext, soft, soft pooled, soft LDS bricks) x primary
+    # index 2 + EXT 5-6 (glass in draw order, hard / soft shadows) x integer index only)
+    assert len(_render(meta)) == 96
 
 
 def test_render_kernels_fit_eight_waves_and_no_arg_copy(meta):
@@ -30,6 +31,15 @@ def test_render_kernels_fit_eight_waves_and_no_arg_copy(meta):
             assert v["vgpr_count"] <= 64 and v["sgpr_count"] <= 80, (p, v)
         elif not p[1]:                                 # EXT 4: LDS bricks hold it to 7 waves/SIMD anyway
             assert v["vgpr_count"] <= 80, (p, v)
+
+
+def test_product_kernels_spill_limits(meta):
+    """The timed instantiations stay within their VGPR spill budgets (kernel_meta.SPILL_LIMITS)."""
+    from voxmap_amd import kernel_meta
+    for p, v in _render(meta).items():
+        lim = kernel_meta.SPILL_LIMITS.get(p[3])
+        if not p[1] and lim is not None:
+            assert v["vgpr_spill_count"] <= lim, (p, v)
 
 
 def test_v1_kernel_has_no_spills(meta):

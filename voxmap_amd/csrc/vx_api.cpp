@@ -50,6 +50,7 @@ struct vx_scene {
     uint32_t *d_rg2 = nullptr;    // AO x-pairs: (R, G) of cells x and x + 1, clamped, (X + 1) per row
     uint8_t *d_bcol = nullptr;    // map.bin's B channel as uploaded (vx_scene_read_field)
     uint16_t *d_qface = nullptr;  // greedy mesh per face: 6 planes of X*Y*Z offsets from the quad origin
+    uint32_t *d_qcopy = nullptr;  // per octant, prim layout: entry faces' offsets (CHUNK <= 32), or null
     int chunk = 0;                // its CHUNK (sdf.cpp:284, voxmap.h:9)
     uint32_t *d_fp2d = nullptr;   // 2D mode: per column vis colour + quad corner (KernelArgs::fp2d)
     std::vector<Quad2d> quads2d;  // 2D mode: the footprint's greedy quads (vx_scene_vertex2d)
@@ -221,6 +222,19 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
             lrc = launch_field_octant(lin, X, Y, Z, cap, oct, ga, gb, s->stream);
             if (!lrc) lrc = launch_field_box(lin, psum, s->d_prim + oct * L.texels, X, Y, Z, L.pad, cap, oct, s->stream);
         }
+        // the fp32-index walk's companion copy: quad offsets loaded beside
+        // every prim word; fields whose walk takes the integer index (or CHUNK > 32) read
+        // the face table once after the walk instead.  Optional: not allocated if it does not fit.
+        const bool f32_ok = 4.0 * (double)L.Xp * (double)L.Yp < 8388608.0 && 32.0 * (double)L.texels < 4294967296.0 &&
+                            L.Zp < (1 << 20);
+        if (!lrc && in.chunk <= 32 && f32_ok) {
+            if (hipMalloc(&s->d_qcopy, 8 * L.texels * 4) != hipSuccess) {
+                (void)hipGetLastError();
+                s->d_qcopy = nullptr;
+            } else {
+                lrc = launch_qcopy(s->d_qface, s->d_qcopy, X, Y, Z, L.pad, L.texels, s->stream);
+            }
+        }
         e = hipStreamSynchronize(s->stream);
     }
     if (psum) (void)hipFree(psum);
@@ -254,6 +268,7 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_noise4) (void)hipFree(s->d_noise4);
     if (s->d_bcol) (void)hipFree(s->d_bcol);
     if (s->d_qface) (void)hipFree(s->d_qface);
+    if (s->d_qcopy) (void)hipFree(s->d_qcopy);
     if (s->d_fp2d) (void)hipFree(s->d_fp2d);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
@@ -457,6 +472,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.noise4 = s->d_noise4;
     a.fp2d = s->d_fp2d;
     a.qface = s->d_qface;
+    a.qcopy = s->d_qcopy;
     a.quad_gbuf = (p->flags & VX_FLAG_UNIT_GBUF) ? 0 : 1;
     a.chunk = s->chunk;
     a.X = s->X; a.Y = s->Y; a.Z = s->Z;
@@ -504,7 +520,8 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
         const bool ok = xy4 < 8388608.0 && 32.0 * (double)s->L.texels < 4294967296.0 &&
                         std::abs(p->cam_cell[0]) < (1 << 21) && std::abs(p->cam_cell[1]) < (1 << 21) &&
                         std::abs(p->cam_cell[2]) < (1 << 20) && s->L.Zp < (1 << 20);   // |z| < 2^21 (k_render)
-        a.prim_f32 = ok && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
+        // (the fp32-index walk loads its quad offsets from the qcopy beside each prim word)
+        a.prim_f32 = ok && s->d_qcopy && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
         a.kx4 = (float)(4 * (p->cam_cell[0] + s->L.pad));
         a.ky = (float)(p->cam_cell[1] + s->L.pad);
         a.kz = 4u * a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);

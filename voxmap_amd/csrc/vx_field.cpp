@@ -129,8 +129,10 @@ int field_build(const uint8_t *color, int X, int Y, int Z, uint8_t *rgba, int n_
 
 // ---- synthetic noise texture in the layout of noise.cpp:34-41 ----------
 // RGB = white noise, A = tileable 10-octave value-noise fBm mapped like
-// noise.cpp:29 (128 + clamp(300 n, -128, 127)).  Used when the real
-// res/noise.bin.gz is not supplied (it is not shipped with this build).
+// noise.cpp:29 (128 + clamp(300 n, -128, 127)).  Used only when a scene is
+// created without a noise texture; the reference's own res/noise.bin.gz ships
+// as voxmap_amd/data/noise.bin.gz and is what the tests, smoke() and bench.py
+// load (SHA-256 pinned, tests/test_reference_pins.py).
 static inline uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
     h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;

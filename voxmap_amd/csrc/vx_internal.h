@@ -85,6 +85,7 @@ struct KernelArgs {
                              // (x, y+1), (x+1, y+1), REPEAT-wrapped
     const uint32_t *fp2d;    // 2D mode: 2 words per column (x fastest): vis colour, quad corner x0 | y0 << 16
     const uint16_t *qface;   // greedy mesh per face: plane n (normal index) of X*Y*Z u16, du | dv << 8 (launch_face_quads)
+    const uint32_t *qcopy;   // 8 copies in the prim layout: the octant's entry faces' offsets (launch_qcopy), or null
     int quad_gbuf;           // 1: fragments carry the quad-relative split (render.vert:25-28); 0: the unit cell
     int chunk;               // the mesh's CHUNK (glass draw order, face_key)
     int X, Y, Z;
@@ -169,6 +170,8 @@ int exit_plan(const FrameConsts &fc, int SB, int *oct, int *kx, int *ky);
 // face's offset from its quad's origin, 0xFFFF = no face; from the upload after launch_field_vis
 int launch_face_quads(const uint32_t *lin, uint16_t *qface, int X, int Y, int Z, int chunk, void *stream);
 int launch_face_quads_interleave(const uint16_t *qface, uint16_t *out, size_t N, void *stream);
+// per ray octant, the entry faces' offsets (10 bits each) in the prim copies' padded layout (CHUNK <= 32)
+int launch_qcopy(const uint16_t *qface, uint32_t *qcopy, int X, int Y, int Z, int pad, size_t texels, void *stream);
 // AO x-pair array from rg: (X + 1) * Y * Z u32 (R, G of two x-neighbours, clamped)
 int launch_ao_pairs(const uint16_t *rg, uint32_t *rg2, int X, int Y, int Z, void *stream);
 // noise quad texture from the RGBA8 noise: 4 planes (A, R, G, B) of each texel's wrapped 2x2 block

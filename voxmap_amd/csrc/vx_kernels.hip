@@ -25,6 +25,10 @@
 
 #include "vx_internal.h"
 
+#ifndef VX_QSPEC
+#define VX_QSPEC 1
+#endif
+
 namespace vx {
 namespace {
 
@@ -648,6 +652,16 @@ __device__ __forceinline__ void quad_offsets(const KernelArgs &a, int ax, int ni
     o2 = ax == 1 ? lo : (ax == 0 ? hi : 0.0f);
 }
 
+// The same offsets from a qcopy word (the octant's entry faces, 10 bits per
+// face axis ax: du | dv << 5, launch_qcopy) -- chunks of at most 32 cells.
+__device__ __forceinline__ void qcopy_offsets(uint32_t w, int ax, float &o0, float &o1, float &o2) {
+    const unsigned q = (w >> (10 * ax)) & 0x3ffu;
+    const float lo = (float)(q & 31u), hi = (float)(q >> 5);
+    o0 = ax == 2 ? lo : (ax == 1 ? hi : 0.0f);
+    o1 = ax == 0 ? lo : (ax == 2 ? hi : 0.0f);
+    o2 = ax == 1 ? lo : (ax == 0 ? hi : 0.0f);
+}
+
 // ---------------- primary visibility ----------------
 // The nearest front face of the greedy mesh of sdf.cpp:281-356 after back-face
 // culling = the first step along the view ray that ENTERS a meshed cell (vis
@@ -733,10 +747,17 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     const unsigned XpYp4 = 4u * a.XpYp;
     const unsigned kz = a.kz - XpYp4 * (unsigned)ip2 + (((unsigned)oct * a.copy_texels) << 2) - 0x4B000000u -
                         (XpYp4 << 22);
+    // QSPEC (the fp32-index path, a.qcopy): every step also loads the cell's
+    // entry-face quad offsets from a.qcopy at the same byte offset (the copy has
+    // the prim layout), so the hit's offsets arrive with its colour instead of
+    // by one more dependent load after the walk (quad_offsets)
+    constexpr bool QSPEC = F32IDX && VX_QSPEC;
+    uint32_t qw = 0, gqw = 0;
     auto fetch = [&](float x, float y, float z) -> uint32_t {
         if (F32IDX) {
             const float xy = __builtin_fmaf(fXp4, y + ky, __builtin_fmaf(4.0f, x, kx4));
             const unsigned off = __umul24(__float_as_uint(z + 12582912.0f), XpYp4) + __float_as_uint(xy) + kz;
+            if (QSPEC) qw = ld_off(a.qcopy, off);
             return ld_off(a.prim, off);
         }
         const int idx = kray + (int)x + __mul24(a.Xp, (int)y) + __mul24((int)a.XpYp, (int)z);
@@ -784,6 +805,7 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
             gmark = 256;
             g0h = h0; g1h = h1; g2h = h2; gt = te;
             gax = e0 ? 0 : (e1 ? 1 : 2);
+            if (QSPEC) gqw = qw;
         }
         stop = (enter && col != kGlass) ? 1 : 0;       // later glass entries: single layer
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
@@ -811,8 +833,14 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     const float hr0 = h0 - hp0, hr1 = h1 - hp1, hr2 = h2 - hp2;
     float gq0 = 0.0f, gq1 = 0.0f, gq2 = 0.0f, hq0 = 0.0f, hq1 = 0.0f, hq2 = 0.0f;
     if (a.quad_gbuf) {
-        if (gl) quad_offsets(a, gax, 2 * gax + (gpos ? 1 : 0), (int)gr0 + cc0, (int)gr1 + cc1, (int)gr2 + cc2, gq0, gq1, gq2);
-        if (hit) quad_offsets(a, hax, 2 * hax + (hpos ? 1 : 0), (int)hr0 + cc0, (int)hr1 + cc1, (int)hr2 + cc2, hq0, hq1, hq2);
+        if (QSPEC) {
+            // the loaded entry-face word of the recorded step: 10 bits per face axis
+            qcopy_offsets(gqw, gax, gq0, gq1, gq2);
+            qcopy_offsets(qw, hax, hq0, hq1, hq2);
+        } else {
+            if (gl) quad_offsets(a, gax, 2 * gax + (gpos ? 1 : 0), (int)gr0 + cc0, (int)gr1 + cc1, (int)gr2 + cc2, gq0, gq1, gq2);
+            if (hit) quad_offsets(a, hax, 2 * hax + (hpos ? 1 : 0), (int)hr0 + cc0, (int)hr1 + cc1, (int)hr2 + cc2, hq0, hq1, hq2);
+        }
     }
     if (gl) {
         const int up = gpos ? 0 : 1;
@@ -1501,10 +1529,11 @@ __device__ __forceinline__ void shade_2d(const KernelArgs &a, float d0, float d1
 }
 
 // Lane = pixel, wave = 8x8 tile, workgroup = 32x8 pixels.
-// EXT: 0 = v1 (the reference's shader), 1 = extensions (REFLECT, ROUGH) with
-// the hard shadow, 2 = extensions with soft shadows (n sun samples), 3 = 2 with
-// the first surface's samples marched by the pooled wave pass
-// (VX_FLAG_SOFT_POOL), 4 = 3 with LDS brick staging (VX_FLAG_SOFT_BRICK).  Each
+// EXT: 0 = v1 (the reference's shader), 1 = extensions (REFLECT, ROUGH,
+// REFLECT_ALL) with the hard shadow, 2 = extensions with soft shadows (n sun
+// samples), 3 = 2 with the first surface's samples marched by the pooled wave
+// pass (VX_FLAG_SOFT_POOL), 4 = 3 with LDS brick staging (VX_FLAG_SOFT_BRICK),
+// 5 / 6 = 1 / 2 with glass in draw order (VX_FLAG_GLASS_ORDER).  Each
 // instantiation carries only its own code and registers; soft shadows in a
 // kernel of their own also keep the sun_k[0] / sun_k[k] addresses apart (a
 // pointer phi between them makes the compiler copy KernelArgs to scratch).
@@ -1530,9 +1559,11 @@ static_assert(kBX == 1 << kBXS && kBY == 1 << kBYS, "block shape");
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
 __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
-    constexpr int XE = EXT >= 3 ? 2 : EXT;     // the shading instantiation (EXT 3/4 shade as 2)
-    constexpr bool kPool = EXT >= 3;           // VX_FLAG_SOFT_POOL: the pooled wave pass
-    constexpr bool kBrick = EXT == 4;          // VX_FLAG_SOFT_BRICK: + LDS brick staging
+    // the shading instantiation: EXT 3/4 shade as 2; 5/6 are 1/2 with glass in draw order
+    constexpr int XE = EXT == 5 ? 1 : (EXT >= 2 ? 2 : EXT);
+    constexpr bool kPool = EXT == 3 || EXT == 4;   // VX_FLAG_SOFT_POOL: the pooled wave pass
+    constexpr bool kBrick = EXT == 4;              // VX_FLAG_SOFT_BRICK: + LDS brick staging
+    constexpr bool kOrder = EXT >= 5;              // VX_FLAG_GLASS_ORDER: every pane in draw order
     __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
     // pooled pass: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
     // the compacted marching fragments' start (fract, cell) and lit counts
@@ -1590,8 +1621,9 @@ void k_render(KernelArgs a) {
         Surf g[2];
         float t_hit;
         const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt, t_hit);
-        // glass in draw order (EXT >= 1 only; launch_render routes such v1 frames to EXT 1)
-        const bool order = XE >= 1 && (F.flags & VX_FLAG_GLASS_ORDER);
+        // glass in draw order: its own instantiations (EXT 5, 6), so the walk over every
+        // pane of a pixel (glass_scan) adds no code or registers to the others
+        constexpr bool order = kOrder;
         int lit0 = -1;
         if (kPool && !inframe) cnt = Counters{};
         if (kPool && F.soft_sg >= 0 && a.sunp) {
@@ -1922,10 +1954,14 @@ __global__ void k_reduce_stats(unsigned long long *stats) {
 
 template <int F, bool S, bool T, int E>
 static void launch_k(const KernelArgs &a, dim3 grid, dim3 block, hipStream_t s) {
-    if (a.prim_f32)
-        hipLaunchKernelGGL((k_render<F, S, T, E, true>), grid, block, 0, s, a);
-    else
+    if constexpr (E >= 5) {           // glass in draw order: the integer primary index only
         hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, block, 0, s, a);
+    } else {
+        if (a.prim_f32)
+            hipLaunchKernelGGL((k_render<F, S, T, E, true>), grid, block, 0, s, a);
+        else
+            hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, block, 0, s, a);
+    }
 }
 
 int launch_render(const KernelArgs &a, int fmt, void *stream) {
@@ -1946,12 +1982,14 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
         return (int)hipGetLastError();
     }
     const bool brick_ok = a.fc.soft_sg >= 0 && a.sunp && a.fc.soft_lg >= 4 && (a.SXp & 3) == 0 && a.SB >= 9;
-    const int ext = a.fc.n_sun > 1 ? ((a.fc.flags & VX_FLAG_SOFT_BRICK) && brick_ok ? 4
+    const bool order = (a.fc.flags & VX_FLAG_GLASS_ORDER) != 0;   // (the pooled / brick passes: not with it)
+    const int ext = a.fc.n_sun > 1 ? (order ? 6 : (a.fc.flags & VX_FLAG_SOFT_BRICK) && brick_ok ? 4
                                       : (a.fc.flags & (VX_FLAG_SOFT_POOL | VX_FLAG_SOFT_BRICK)) ? 3 : 2)
-                                   : ((a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH | VX_FLAG_GLASS_ORDER |
-                                                     VX_FLAG_REFLECT_ALL)) ? 1 : 0);
+                                   : (order ? 5 : (a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH |
+                                                                 VX_FLAG_REFLECT_ALL)) ? 1 : 0);
 #define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
-#define VX_LE(F, S, T) do { if (ext == 4) VX_L(F, S, T, 4); else if (ext == 3) VX_L(F, S, T, 3); \
+#define VX_LE(F, S, T) do { if (ext == 6) VX_L(F, S, T, 6); else if (ext == 5) VX_L(F, S, T, 5); \
+                                else if (ext == 4) VX_L(F, S, T, 4); else if (ext == 3) VX_L(F, S, T, 3); \
                                 else if (ext == 2) VX_L(F, S, T, 2); \
                                 else if (ext) VX_L(F, S, T, 1); else VX_L(F, S, T, 0); } while (0)
 #define VX_LT(F, S) do { if (tiled) VX_LE(F, S, true); else VX_LE(F, S, false); } while (0)
@@ -2132,6 +2170,27 @@ __global__ __launch_bounds__(64) void k_face_quads(const uint32_t *lin, uint16_t
                 }
             i += w - 1;
         }
+}
+// Per ray octant, a copy in the prim layout (padded, pad = P) of each cell's
+// entry faces' quad offsets: a ray of octant oct (bit i: negative along i)
+// enters a cell through the face with normal index 2a + (positive ? 1 : 0) on
+// axis a; word = sum over a of (du | dv << 5) << 10a (CHUNK <= 32), 0 where the
+// face does not exist (as quad_offsets) and on the border.  The fp32-index
+// primary walk loads it beside every prim word (QSPEC).
+__global__ void k_qcopy(const uint16_t *qf, uint32_t *dst, int X, int Y, int Z, int P, int oct, size_t N) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int x = (int)(i % X), y = (int)((i / X) % Y), z = (int)(i / ((size_t)X * Y));
+    uint32_t w = 0;
+#pragma unroll
+    for (int ax = 0; ax < 3; ax++) {
+        const int nidx = 2 * ax + (((oct >> ax) & 1) ? 0 : 1);
+        unsigned q = qf[(size_t)nidx * N + i];
+        q = q == 0xFFFFu ? 0u : q;
+        w |= ((q & 31u) | (((q >> 8) & 31u) << 5)) << (10 * ax);
+    }
+    const size_t Xp = (size_t)X + 2 * P, Yp = (size_t)Y + 2 * P;
+    dst[(size_t)(x + P) + Xp * ((size_t)(y + P) + Yp * (size_t)(z + P))] = w;
 }
 // the table in the oracle's layout (6 per cell) for vx_scene_read_face_quads
 __global__ void k_face_quads_interleave(const uint16_t *qf, uint16_t *out, size_t N) {
@@ -2337,6 +2396,17 @@ int launch_face_quads(const uint32_t *lin, uint16_t *qface, int X, int Y, int Z,
     if (blocks >= (1ull << 31)) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(k_face_quads, dim3((unsigned)blocks), dim3(64), (size_t)chunk * chunk, s, lin, qface, X, Y, Z,
                        chunk, ncy, ncz, N);
+    return (int)hipGetLastError();
+}
+
+int launch_qcopy(const uint16_t *qface, uint32_t *qcopy, int X, int Y, int Z, int pad, size_t texels, void *stream) {
+    const size_t N = (size_t)X * Y * Z;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(qcopy, 0, 8 * texels * 4, s);
+    if (e != hipSuccess) return (int)e;
+    for (int o = 0; o < 8; o++)
+        hipLaunchKernelGGL(k_qcopy, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, qface, qcopy + o * texels, X,
+                           Y, Z, pad, o, N);
     return (int)hipGetLastError();
 }
 

@@ -22,6 +22,9 @@ FIELDS = ("private_segment_fixed_size", "vgpr_count", "sgpr_count", "vgpr_spill_
           "group_segment_fixed_size")
 RENDER_SCRATCH_LIMIT = 256      # bytes per thread: spill slots yes, a KernelArgs copy (~1.7 KB) no
 STATS_SCRATCH_LIMIT = 512       # the counting (STATS) instantiations keep ~16 counters live: more spill slots
+# VGPR spills allowed per EXT mode of a timed (non-STATS) k_render instantiation
+# (0 v1, 1 extensions, 2 soft shadows, 3 pooled, 4 LDS bricks, 5/6 glass in draw order)
+SPILL_LIMITS = {0: 0, 1: 0, 2: 4, 3: 4, 4: 40}
 RENDER_VGPR_LIMIT = 64          # 8 waves/SIMD
 
 
@@ -86,6 +89,11 @@ def check(lib: str) -> dict[str, dict[str, int]]:
         lim = STATS_SCRATCH_LIMIT if stats else RENDER_SCRATCH_LIMIT
         if v.get("private_segment_fixed_size", 0) > lim:
             bad.append(f"{name}: private segment {v['private_segment_fixed_size']} B > {lim}")
+        # the timed product kernels: v1 and the extensions spill-free, soft shadows a
+        # few VGPRs (scratch traffic in the hot path doubled the EXT 1 frame once)
+        spill_lim = SPILL_LIMITS.get(p[3]) if p is not None and not stats else None
+        if spill_lim is not None and v.get("vgpr_spill_count", 0) > spill_lim:
+            bad.append(f"{name}: {v['vgpr_spill_count']} VGPRs spilled > {spill_lim}")
         if not stats and v.get("vgpr_count", 0) > (80 if brick else RENDER_VGPR_LIMIT):
             bad.append(f"{name}: {v['vgpr_count']} VGPRs > {RENDER_VGPR_LIMIT}")
     if bad:
