@@ -116,6 +116,9 @@ extern "C" {
  * (DESIGN.md §3 "Extensions"; README.md:18-25 describes a reflection pass over
  * the frame).  What a pane blends over is seen through the glass: not mirrored. */
 #define VX_FLAG_REFLECT_ALL 0x2000u
+/* Diagnostics (ABI 8): the frame's 32x8-pixel blocks dispatched bottom row first
+ * (the launch's tail).  Identical frames. */
+#define VX_FLAG_ROWS_BOTTOM_UP 0x4000u
 #define VX_MAX_SHADOW_SAMPLES 16
 
 typedef struct vx_scene vx_scene;

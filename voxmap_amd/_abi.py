@@ -33,7 +33,8 @@ FLAG_NO_EXIT = 0x200                            # diagnostics: march without the
 FLAG_NO_CONE = 0x400                            # diagnostics: orthant exit tables only (same frames)
 FLAG_UNIT_GBUF = 0x800                          # diagnostics: the unit-cell G-buffer split (ABI <= 7)
 FLAG_GLASS_ORDER = 0x1000                       # every pane in draw order (render.js:82-91), not one layer
-FLAG_REFLECT_ALL = 0x2000                       # ext: every primary fragment mirrors the scene
+FLAG_REFLECT_ALL = 0x2000                       # ext: every first surface mirrors the scene
+FLAG_ROWS_BOTTOM_UP = 0x4000                    # diagnostics: blocks dispatched bottom row first (same frames)
 MAX_GLASS_LAYERS = 8
 MAX_SHADOW_SAMPLES = 16
 ABI_VERSION = 8

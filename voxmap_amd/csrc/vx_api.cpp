@@ -67,6 +67,8 @@ struct vx_scene {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     FieldLayout L;
+    unsigned long long *d_blk = nullptr;   // VX_BLOCK_TIMING builds: the last launch's block times
+    size_t blk_cap = 0, blk_n = 0;
 };
 
 #define VX_HIP(call)                                                                                 \
@@ -144,7 +146,6 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMalloc(&s->d_noise4, 4 * noise_bytes)) != hipSuccess ||
         (e = hipMalloc(&s->d_stats, sizeof(unsigned long long) * ST_COUNT * 64)) != hipSuccess ||
         (e = hipMalloc(&s->d_bcol, field_bytes / 4)) != hipSuccess ||
-        (e = hipMalloc(&s->d_qface, 3 * field_bytes)) != hipSuccess ||
         (e = hipMalloc(&ga, field_bytes / 4)) != hipSuccess || (e = hipMalloc(&gb, field_bytes / 4)) != hipSuccess ||
         (!from_grid &&
          (e = hipMemcpyAsync(lin, field.data(), field_bytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess) ||
@@ -180,8 +181,6 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         (e = hipMemsetD32Async((hipDeviceptr_t)s->d_prim, 0xFFFFFFFF, 8 * L.texels, s->stream)) == hipSuccess) {
         // B -> vis colour first: the boxes and prim copies classify by it
         lrc = launch_field_vis(lin, s->d_bcol, X, Y, Z, s->stream);
-        // the greedy mesh's quad per face (render.vert:25-28: v_cellPos is the quad origin)
-        if (!lrc) lrc = launch_face_quads(lin, s->d_qface, X, Y, Z, in.chunk, s->stream);
         if (!lrc) lrc = build_2d(s, lin);
         if (!lrc) lrc = launch_field_pack(lin, s->d_sun, s->d_rg, X, Y, Z, s->stream);
         if (!lrc) lrc = launch_ao_pairs(s->d_rg, s->d_rg2, X, Y, Z, s->stream);
@@ -222,12 +221,25 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
             lrc = launch_field_octant(lin, X, Y, Z, cap, oct, ga, gb, s->stream);
             if (!lrc) lrc = launch_field_box(lin, psum, s->d_prim + oct * L.texels, X, Y, Z, L.pad, cap, oct, s->stream);
         }
+        // the greedy mesh's quad per face (render.vert:25-28: v_cellPos is the quad origin),
+        // allocated after the arrays the kernels read every step: placed in front of them
+        // it moved their device addresses, and the v1 frame measured 3.3 % slower with the
+        // same kernel code (profiles/r04_ab_v1_bisect.txt, r04_ab_alloc_order.txt)
+        if (!lrc) {
+            if ((e = hipMalloc(&s->d_qface, 3 * field_bytes)) == hipSuccess)
+                lrc = launch_face_quads(lin, s->d_qface, X, Y, Z, in.chunk, s->stream);
+            else
+                lrc = (int)e;
+        }
         // the fp32-index walk's companion copy: quad offsets loaded beside
         // every prim word; fields whose walk takes the integer index (or CHUNK > 32) read
         // the face table once after the walk instead.  Optional: not allocated if it does not fit.
         const bool f32_ok = 4.0 * (double)L.Xp * (double)L.Yp < 8388608.0 && 32.0 * (double)L.texels < 4294967296.0 &&
                             L.Zp < (1 << 20);
-        if (!lrc && in.chunk <= 32 && f32_ok) {
+#ifndef VX_QSPEC
+#define VX_QSPEC 1
+#endif
+        if (VX_QSPEC && !lrc && in.chunk <= 32 && f32_ok) {
             if (hipMalloc(&s->d_qcopy, 8 * L.texels * 4) != hipSuccess) {
                 (void)hipGetLastError();
                 s->d_qcopy = nullptr;
@@ -269,6 +281,7 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_bcol) (void)hipFree(s->d_bcol);
     if (s->d_qface) (void)hipFree(s->d_qface);
     if (s->d_qcopy) (void)hipFree(s->d_qcopy);
+    if (s->d_blk) (void)hipFree(s->d_blk);
     if (s->d_fp2d) (void)hipFree(s->d_fp2d);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
@@ -306,6 +319,18 @@ static int read_copy(vx_scene *s, int octant, void *host_out, size_t cap, bool b
     if (e != hipSuccess) return set_error(VX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
     return VX_OK;
 }
+
+#ifdef VX_BLOCK_TIMING
+// diagnostics build only: the last untiled launch's per-block (start, end) on the 100 MHz clock
+int vx_debug_block_times(vx_scene *s, unsigned long long *out, size_t cap, size_t *n) {
+    if (!s || !n) return set_error(VX_EINVAL, "vx_debug_block_times: null argument");
+    *n = s->blk_n;
+    if (!out || !s->d_blk) return VX_OK;
+    VX_HIP(hipDeviceSynchronize());
+    VX_HIP(hipMemcpy(out, s->d_blk, 16 * std::min(cap / 2, s->blk_n), hipMemcpyDeviceToHost));
+    return VX_OK;
+}
+#endif
 
 int vx_scene_read_face_quads(vx_scene *s, void *host_out, size_t cap) {
     if (!s || !host_out) return set_error(VX_EINVAL, "vx_scene_read_face_quads: null argument");
@@ -521,7 +546,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
                         std::abs(p->cam_cell[0]) < (1 << 21) && std::abs(p->cam_cell[1]) < (1 << 21) &&
                         std::abs(p->cam_cell[2]) < (1 << 20) && s->L.Zp < (1 << 20);   // |z| < 2^21 (k_render)
         // (the fp32-index walk loads its quad offsets from the qcopy beside each prim word)
-        a.prim_f32 = ok && s->d_qcopy && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
+        a.prim_f32 = ok && (s->d_qcopy || !VX_QSPEC) && !(p->flags & VX_FLAG_INT_INDEX) ? 1 : 0;
         a.kx4 = (float)(4 * (p->cam_cell[0] + s->L.pad));
         a.ky = (float)(p->cam_cell[1] + s->L.pad);
         a.kz = 4u * a.XpYp * (unsigned)(p->cam_cell[2] + s->L.pad);
@@ -531,6 +556,18 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
         a.stats = s->d_stats;
         VX_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(unsigned long long) * ST_COUNT * 64, st));
     }
+#ifdef VX_BLOCK_TIMING
+    if (!ts.ids) {
+        const size_t nb = (size_t)((w + 31) / 32) * (size_t)((h + 7) / 8);
+        if (nb > s->blk_cap) {
+            if (s->d_blk) VX_HIP(hipFree(s->d_blk));
+            VX_HIP(hipMalloc(&s->d_blk, 16 * nb));
+            s->blk_cap = nb;
+        }
+        s->blk_n = nb;
+        a.blk_time = s->d_blk;
+    }
+#endif
     // events only for the stats launch (kernel_ms): two extra stream packets
     // per frame otherwise widen the gap between back-to-back frames
     if (stats) VX_HIP(hipEventRecord(s->ev0, st));

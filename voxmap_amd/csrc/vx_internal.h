@@ -88,6 +88,7 @@ struct KernelArgs {
     const uint32_t *qcopy;   // 8 copies in the prim layout: the octant's entry faces' offsets (launch_qcopy), or null
     int quad_gbuf;           // 1: fragments carry the quad-relative split (render.vert:25-28); 0: the unit cell
     int chunk;               // the mesh's CHUNK (glass draw order, face_key)
+    unsigned long long *blk_time;   // diagnostics build (VX_BLOCK_TIMING): per block start, end; else null
     int X, Y, Z;
     int noise_w, noise_h;    // powers of two
     float noise_rw, noise_rh;    // 1/noise_w, 1/noise_h (exact)

@@ -832,7 +832,11 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     const float gr0 = g0h - hp0, gr1 = g1h - hp1, gr2 = g2h - hp2;   // relative cells
     const float hr0 = h0 - hp0, hr1 = h1 - hp1, hr2 = h2 - hp2;
     float gq0 = 0.0f, gq1 = 0.0f, gq2 = 0.0f, hq0 = 0.0f, hq1 = 0.0f, hq2 = 0.0f;
+#ifdef VX_NO_QUAD
+    if (false) {
+#else
     if (a.quad_gbuf) {
+#endif
         if (QSPEC) {
             // the loaded entry-face word of the recorded step: 10 bits per face axis
             qcopy_offsets(gqw, gax, gq0, gq1, gq2);
@@ -1148,6 +1152,12 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, float d0, float d
     sx = sx * 0.1f; sy = sy * 0.1f;
     const float sl = sqrtf(sqrtf(sx * sx + sy * sy));
     sx = sx * sl; sy = sy * sl;
+    // render.frag:184-203 computes both the clouds and the mountains and keeps
+    // one (:199-203).  The three samples that decide or feed the first step of
+    // either (the mountain height, the two cloud warps) load together; then only
+    // the kept branch's last sample is taken (the mountain factor or the cloud
+    // factor): the same values, one noise sample less per sky pixel.
+#ifdef VX_OLD_SKY
     const float n0 = fbm(a, 2.0f * sx + ct, 2.0f * sy + ct);
     const float n1 = fbm(a, 2.0f * sx - ct, 2.0f * sy - ct);
     sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
@@ -1168,6 +1178,28 @@ __device__ __forceinline__ void shade_sky(const KernelArgs &a, float d0, float d
 #pragma unroll
         for (int i = 0; i < 3; i++) sky[i] = gmix(sky[i], gmix(sunCol[i], 0.8f, scf), cloudFactor);
     }
+#else
+    const float n0 = fbm(a, 2.0f * sx + ct, 2.0f * sy + ct);
+    const float n1 = fbm(a, 2.0f * sx - ct, 2.0f * sy - ct);
+    const float mountainPos = r0 / r1;                                            // :195
+    float mountainHeight = 1.0f - fbm(a, 0.3f * mountainPos, 0.3f * mountainPos);
+    mountainHeight = mountainHeight / (vexp(0.3f * mountainPos * mountainPos) * 6.0f);
+    if (mountainHeight > r2 && r1 > 0.0f && r2 > 0.0f) {
+        const float mountainFactor = 2.0f - fbm(a, 2.0f * (mountainPos + r1), 2.0f * (mountainPos + r2));
+        const float mt[3] = {0.7f, 0.8f, 0.7f};
+        const float w = mountainFactor * r2;
+#pragma unroll
+        for (int i = 0; i < 3; i++) sky[i] = gmix(sky[i], sky[i] * mt[i], w);
+    } else {
+        sx = sx * (3.0f + n0); sy = sy * (3.0f + n1);
+        sx = sx + F.skyOff[0];
+        sy = sy + F.skyOff[1];
+        const float cloudFactor = vexp2(6.0f * (fbm(a, sx + 2.0f * ct, sy + -9.0f * ct) - 1.0f));
+        const float scf = sqrtf(cloudFactor);
+#pragma unroll
+        for (int i = 0; i < 3; i++) sky[i] = gmix(sky[i], gmix(sunCol[i], 0.8f, scf), cloudFactor);
+    }
+#endif
     o[0] = sky[0]; o[1] = sky[1]; o[2] = sky[2]; o[3] = 1.0f;
 }
 
@@ -1559,11 +1591,12 @@ static_assert(kBX == 1 << kBXS && kBY == 1 << kBYS, "block shape");
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
 __global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
-    // the shading instantiation: EXT 3/4 shade as 2; 5/6 are 1/2 with glass in draw order
+    // the shading instantiation: EXT 3/4 shade as 2; 5/6 are 1/2 with the general
+    // shading block (glass in draw order, REFLECT_ALL)
     constexpr int XE = EXT == 5 ? 1 : (EXT >= 2 ? 2 : EXT);
     constexpr bool kPool = EXT == 3 || EXT == 4;   // VX_FLAG_SOFT_POOL: the pooled wave pass
     constexpr bool kBrick = EXT == 4;              // VX_FLAG_SOFT_BRICK: + LDS brick staging
-    constexpr bool kOrder = EXT >= 5;              // VX_FLAG_GLASS_ORDER: every pane in draw order
+    constexpr bool kGeneral = EXT >= 5;            // VX_FLAG_GLASS_ORDER / VX_FLAG_REFLECT_ALL
     __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
     // pooled pass: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
     // the compacted marching fragments' start (fract, cell) and lit counts
@@ -1602,12 +1635,18 @@ void k_render(KernelArgs a) {
         oy = (tid / a.tiles_x) * a.tile_h + ty0;
     } else {
         ox = blockIdx.x << kBXS;
-        oy = blockIdx.y << kBYS;
+        // diagnostics (VX_FLAG_ROWS_BOTTOM_UP): block rows dispatched bottom row first
+        oy = ((a.fc.flags & VX_FLAG_ROWS_BOTTOM_UP) ? gridDim.y - 1 - blockIdx.y : blockIdx.y) << kBYS;
     }
     const int px = ox + lx, py = oy + ly;
     const bool inframe = px < a.w && py < a.h;
     const FrameConsts &F = a.fc;
     Counters cnt = {};
+#ifdef VX_BLOCK_TIMING
+    // diagnostics build only (tools/block_times.py): the block's start and end
+    // on the 100 MHz constant clock
+    const unsigned long long t_blk0 = __builtin_amdgcn_s_memrealtime();
+#endif
     unsigned n_sky = 0, n_block = 0, n_glass = 0, n_px = 0;
     // The pooled pass deals work over all 64 lanes of a wave, so there every
     // lane runs: a lane off the frame (a partial edge wave) takes the nearest
@@ -1621,9 +1660,11 @@ void k_render(KernelArgs a) {
         Surf g[2];
         float t_hit;
         const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt, t_hit);
-        // glass in draw order: its own instantiations (EXT 5, 6), so the walk over every
-        // pane of a pixel (glass_scan) adds no code or registers to the others
-        constexpr bool order = kOrder;
+        // glass in draw order and REFLECT_ALL: instantiations of their own (EXT 5, 6), so
+        // the walk over every pane of a pixel (glass_scan) and the mirror walk of every
+        // surface add no code or registers to the others (one shading loop there, the
+        // reference's single site here: measured 4 % on C3 full quality when shared)
+        const bool order = kGeneral && (F.flags & VX_FLAG_GLASS_ORDER);
         int lit0 = -1;
         if (kPool && !inframe) cnt = Counters{};
         if (kPool && F.soft_sg >= 0 && a.sunp) {
@@ -1740,6 +1781,34 @@ void k_render(KernelArgs a) {
                 // itself would be: 9 registers, spilled to scratch at the
                 // 64-VGPR budget).  Shading has no side effects besides the
                 // counters (sums), so the order changes no result.
+if constexpr (!kGeneral) {
+                float dst[4];
+                if (g[0].id == 2) {
+                    if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
+                    else shade_sky(a, d0, d1, d2, dst, cnt);
+                }
+                float rd[3];
+                shade_block<XE>(a, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
+                if (g[0].id == 2) {
+                    n_glass = 1;
+                    if (XE && (F.flags & VX_FLAG_REFLECT)) {
+                        float refl[3];
+                        reflect_color<XE>(a, g[0], rd, refl, cnt);
+                        const int ax = g[0].nidx >> 1;
+                        const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
+                        const float x = 1.0f - cs, x2 = x * x;
+                        const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
+#pragma unroll
+                        for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
+                    }
+                    const float al = rgba[3];
+#pragma unroll
+                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+                } else {
+                    n_block = 1;
+                }
+                (void)t_hit;
+} else {
                 float dst[4];
                 const bool glass = g[0].id == 2;
                 if (glass) {
@@ -1787,6 +1856,7 @@ void k_render(KernelArgs a) {
                 } else {
                     n_block = 1;
                 }
+}
             }
             rgba[3] = 1.0f;
             if (FMT == VX_PIXEL_RGBA8)
@@ -1805,6 +1875,14 @@ void k_render(KernelArgs a) {
             reinterpret_cast<uint32_t *>(a.out)[out_index<TILED>(a, tile_k, tx0 + sx, ty0 + sy, ox + sx, oy + sy)] =
                 s_px[sy][sx];
     }
+#ifdef VX_BLOCK_TIMING
+    __syncthreads();
+    if (threadIdx.x == 0 && a.blk_time) {
+        const size_t b = (size_t)blockIdx.x + (size_t)blockIdx.y * gridDim.x;
+        a.blk_time[2 * b] = t_blk0;
+        a.blk_time[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     if (STATS) {
         unsigned long long v[ST_COUNT];
         v[ST_PIXELS] = wave_sum(n_px);
@@ -1982,12 +2060,18 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
         return (int)hipGetLastError();
     }
     const bool brick_ok = a.fc.soft_sg >= 0 && a.sunp && a.fc.soft_lg >= 4 && (a.SXp & 3) == 0 && a.SB >= 9;
-    const bool order = (a.fc.flags & VX_FLAG_GLASS_ORDER) != 0;   // (the pooled / brick passes: not with it)
-    const int ext = a.fc.n_sun > 1 ? (order ? 6 : (a.fc.flags & VX_FLAG_SOFT_BRICK) && brick_ok ? 4
+    // the general shading block (glass in draw order, REFLECT_ALL): EXT 5 / 6 (not with the pooled pass)
+    const bool general = (a.fc.flags & (VX_FLAG_GLASS_ORDER | VX_FLAG_REFLECT_ALL)) != 0;
+    const int ext = a.fc.n_sun > 1 ? (general ? 6 : (a.fc.flags & VX_FLAG_SOFT_BRICK) && brick_ok ? 4
                                       : (a.fc.flags & (VX_FLAG_SOFT_POOL | VX_FLAG_SOFT_BRICK)) ? 3 : 2)
-                                   : (order ? 5 : (a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH |
-                                                                 VX_FLAG_REFLECT_ALL)) ? 1 : 0);
+                                   : (general ? 5 : (a.fc.flags & (VX_FLAG_REFLECT | VX_FLAG_ROUGH)) ? 1 : 0);
 #define VX_L(F, S, T, E) launch_k<F, S, T, E>(a, grid, block, s)
+#ifdef VX_AB_LEAN
+    // A/B timing variants (tools/abtime.py): untiled RGBA8 without stats only, EXT 0-3
+    if (fmt != VX_PIXEL_RGBA8 || st || tiled || ext > 3) return (int)hipErrorNotSupported;
+    if (ext == 3) VX_L(1, false, false, 3); else if (ext == 2) VX_L(1, false, false, 2);
+    else if (ext) VX_L(1, false, false, 1); else VX_L(1, false, false, 0);
+#else
 #define VX_LE(F, S, T) do { if (ext == 6) VX_L(F, S, T, 6); else if (ext == 5) VX_L(F, S, T, 5); \
                                 else if (ext == 4) VX_L(F, S, T, 4); else if (ext == 3) VX_L(F, S, T, 3); \
                                 else if (ext == 2) VX_L(F, S, T, 2); \
@@ -1995,8 +2079,9 @@ int launch_render(const KernelArgs &a, int fmt, void *stream) {
 #define VX_LT(F, S) do { if (tiled) VX_LE(F, S, true); else VX_LE(F, S, false); } while (0)
     if (fmt == VX_PIXEL_RGBA32F) { if (st) VX_LT(0, true); else VX_LT(0, false); }
     else { if (st) VX_LT(1, true); else VX_LT(1, false); }
-#undef VX_LT
 #undef VX_LE
+#undef VX_LT
+#endif
 #undef VX_L
     if (st) hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(64), 0, s, a.stats);
     return (int)hipGetLastError();
