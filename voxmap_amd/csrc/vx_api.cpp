@@ -39,11 +39,14 @@ struct vx_scene {
         hipEvent_t ready = nullptr;
         unsigned long long used = 0;
         // one event per stream that enqueued a render reading this copy since it
-        // was built (recorded after the launch, under cone_mu): recycling the slot
-        // waits for exactly those readers
+        // was built (recorded after the launch, under cone_mu, once the scene
+        // has seen a second stream): recycling the slot waits for exactly those
+        // readers
         std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
     } cones[2];
     unsigned long long cone_tick = 0;
+    hipStream_t first_st = nullptr;   // the one stream cone copies were used on so far
+    bool any_st = false, multi_st = false;
     std::mutex cone_mu;
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
@@ -400,7 +403,8 @@ struct TileSpec {
 // The frame's cone copy {oct, kx, ky}: found in the scene's cache (the
 // stream waits for its build), or built on stream st into a free or the least
 // recently used slot -- after every render enqueued so far that reads that
-// slot has finished (its readers' events).  The caller holds s->cone_mu from
+// slot has finished (its readers' events; stream order while the scene is used
+// from one stream, cone_stream).  The caller holds s->cone_mu from
 // here until its render is enqueued and recorded as a reader (note_reader), so
 // no other thread can recycle the slot in between.  t_build: recorded on st
 // just before the build's first packet (vx_prepare_sun's timing), if built.
@@ -429,8 +433,8 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         VX_HIP(hipEventRecord(slot->ready, st));
         slot->oct = oct; slot->kx = kx; slot->ky = ky;
         *built = true;
-    } else {
-        VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));
+    } else if (s->multi_st) {
+        VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));   // one stream: built before, in stream order
     }
     slot->used = ++s->cone_tick;
     *out = slot->d;
@@ -438,8 +442,29 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
     return VX_OK;
 }
 
-// After a render reading cone copy c was enqueued on st (cone_mu held): record it as a reader.
-static int note_reader(vx_scene::Cone *c, hipStream_t st) {
+// Before a lookup on stream st (cone_mu held).  While every lookup of the
+// scene comes from one stream, readers need no events: a slot rebuilt on that
+// stream follows the renders that read it in stream order (and an event per
+// render is one more stream packet between back-to-back frames: +3 % at C3).
+// The first lookup from a second stream switches the scene to per-render
+// reader events, after one device-wide wait for the readers enqueued without.
+static int cone_stream(vx_scene *s, hipStream_t st) {
+    if (s->multi_st) return VX_OK;
+    if (!s->any_st) {
+        s->any_st = true;
+        s->first_st = st;
+        return VX_OK;
+    }
+    if (st == s->first_st) return VX_OK;
+    VX_HIP(hipDeviceSynchronize());
+    s->multi_st = true;
+    return VX_OK;
+}
+
+// After a render reading cone copy c was enqueued on st (cone_mu held): record
+// it as a reader (scenes used from more than one stream).
+static int note_reader(vx_scene *s, vx_scene::Cone *c, hipStream_t st) {
+    if (!s->multi_st) return VX_OK;
     for (auto &r : c->readers)
         if (r.first == st) {
             VX_HIP(hipEventRecord(r.second, st));
@@ -524,7 +549,9 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     std::unique_lock<std::mutex> cone_lock(s->cone_mu);
     vx_scene::Cone *cone = nullptr;
     {
-        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
+        int rc = cone_stream(s, st);
+        if (rc) return rc;
+        rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
         if (rc) return rc;
     }
     if (!cone) cone_lock.unlock();
@@ -574,7 +601,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     int rc = launch_render(a, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("render launch failed: ") + hipGetErrorString((hipError_t)rc));
     if (cone) {
-        rc = note_reader(cone, st);
+        rc = note_reader(s, cone, st);
         cone_lock.unlock();
         if (rc) return rc;
     }
@@ -606,6 +633,8 @@ int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_
         // ev0 is recorded inside cone_copy right before the build's first packet:
         // build_ms is the copy's GPU time, not the host's allocation or waits
         std::lock_guard<std::mutex> lock(s->cone_mu);
+        rc = cone_stream(s, st);
+        if (rc) return rc;
         rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, s->ev0);
         if (rc) return rc;
         if (built) VX_HIP(hipEventRecord(s->ev1, st));
