@@ -838,8 +838,9 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     if (a.quad_gbuf) {
 #endif
         if (QSPEC) {
-            // the loaded entry-face word of the recorded step: 10 bits per face axis
-            qcopy_offsets(gqw, gax, gq0, gq1, gq2);
+            // the loaded entry-face word of the recorded step: 10 bits per face
+            // axis (the glass record's only in a wave that has one: most have none)
+            if (__ballot(gl) != 0) qcopy_offsets(gqw, gax, gq0, gq1, gq2);
             qcopy_offsets(qw, hax, hq0, hq1, hq2);
         } else {
             if (gl) quad_offsets(a, gax, 2 * gax + (gpos ? 1 : 0), (int)gr0 + cc0, (int)gr1 + cc1, (int)gr2 + cc2, gq0, gq1, gq2);
