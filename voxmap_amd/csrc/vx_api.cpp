@@ -38,11 +38,7 @@ struct vx_scene {
         int8_t *d = nullptr;
         hipEvent_t ready = nullptr;
         unsigned long long used = 0;
-        // one event per stream that enqueued a render reading this copy since it
-        // was built (recorded after the launch, under cone_mu, once the scene
-        // has seen a second stream): recycling the slot waits for exactly those
-        // readers
-        std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
+        bool ready_seen = false;      // the build's `ready` event observed complete
     } cones[2];
     unsigned long long cone_tick = 0;
     hipStream_t first_st = nullptr;   // the one stream cone copies were used on so far
@@ -276,7 +272,6 @@ void vx_scene_destroy(vx_scene *s) {
     for (auto &c : s->cones) {
         if (c.d) (void)hipFree(c.d);
         if (c.ready) (void)hipEventDestroy(c.ready);
-        for (auto &r : c.readers) (void)hipEventDestroy(r.second);
     }
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_rg2) (void)hipFree(s->d_rg2);
@@ -401,13 +396,19 @@ struct TileSpec {
 };
 
 // The frame's cone copy {oct, kx, ky}: found in the scene's cache (the
-// stream waits for its build), or built on stream st into a free or the least
+// stream waits for its build unless that is known complete or was enqueued on
+// the same single stream), or built on stream st into a free or the least
 // recently used slot -- after every render enqueued so far that reads that
-// slot has finished (its readers' events; stream order while the scene is used
-// from one stream, cone_stream).  The caller holds s->cone_mu from
-// here until its render is enqueued and recorded as a reader (note_reader), so
-// no other thread can recycle the slot in between.  t_build: recorded on st
-// just before the build's first packet (vx_prepare_sun's timing), if built.
+// slot has finished.  The caller holds s->cone_mu from here until its render
+// is enqueued, so every reader of a slot is enqueued before anyone can recycle
+// it; the recycle then waits for them by stream order (a scene used from one
+// stream, cone_stream) or one device-wide wait (several streams).  No reader
+// is tracked per render: an event recorded after every render is one more
+// stream packet between back-to-back frames, +3 % at C3
+// (profiles/r04_ab_event_c3.txt, r04_ab_multistream_events.txt), while a
+// recycle needs a third sun window in the scene's two slots.  t_build:
+// recorded on st just before the build's first packet (vx_prepare_sun's
+// timing), if built.
 static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built,
                      vx_scene::Cone **used, hipEvent_t t_build) {
     *built = false;
@@ -419,7 +420,7 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         for (auto &c : s->cones)
             if (!c.d || c.used < slot->used) slot = &c;
         if (slot->d) {
-            for (auto &r : slot->readers) VX_HIP(hipEventSynchronize(r.second));
+            if (s->multi_st) VX_HIP(hipDeviceSynchronize());
         } else {
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
             VX_HIP(hipMalloc(&slot->d, np));
@@ -431,10 +432,14 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         const int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
         if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
         VX_HIP(hipEventRecord(slot->ready, st));
+        slot->ready_seen = false;
         slot->oct = oct; slot->kx = kx; slot->ky = ky;
         *built = true;
-    } else if (s->multi_st) {
-        VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));   // one stream: built before, in stream order
+    } else if (s->multi_st && !slot->ready_seen) {       // one stream: built before it, in stream order
+        const hipError_t q = hipEventQuery(slot->ready);
+        if (q == hipSuccess) slot->ready_seen = true;
+        else if (q == hipErrorNotReady) VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));
+        else VX_HIP(q);
     }
     slot->used = ++s->cone_tick;
     *out = slot->d;
@@ -442,12 +447,8 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
     return VX_OK;
 }
 
-// Before a lookup on stream st (cone_mu held).  While every lookup of the
-// scene comes from one stream, readers need no events: a slot rebuilt on that
-// stream follows the renders that read it in stream order (and an event per
-// render is one more stream packet between back-to-back frames: +3 % at C3).
-// The first lookup from a second stream switches the scene to per-render
-// reader events, after one device-wide wait for the readers enqueued without.
+// Before a lookup on stream st (cone_mu held): is the scene still used from
+// one stream only (cone_copy's waits)?
 static int cone_stream(vx_scene *s, hipStream_t st) {
     if (s->multi_st) return VX_OK;
     if (!s->any_st) {
@@ -455,25 +456,7 @@ static int cone_stream(vx_scene *s, hipStream_t st) {
         s->first_st = st;
         return VX_OK;
     }
-    if (st == s->first_st) return VX_OK;
-    VX_HIP(hipDeviceSynchronize());
-    s->multi_st = true;
-    return VX_OK;
-}
-
-// After a render reading cone copy c was enqueued on st (cone_mu held): record
-// it as a reader (scenes used from more than one stream).
-static int note_reader(vx_scene *s, vx_scene::Cone *c, hipStream_t st) {
-    if (!s->multi_st) return VX_OK;
-    for (auto &r : c->readers)
-        if (r.first == st) {
-            VX_HIP(hipEventRecord(r.second, st));
-            return VX_OK;
-        }
-    hipEvent_t e = nullptr;
-    VX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->readers.emplace_back(st, e);
-    VX_HIP(hipEventRecord(e, st));
+    if (st != s->first_st) s->multi_st = true;
     return VX_OK;
 }
 
@@ -600,11 +583,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     if (stats) VX_HIP(hipEventRecord(s->ev0, st));
     int rc = launch_render(a, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("render launch failed: ") + hipGetErrorString((hipError_t)rc));
-    if (cone) {
-        rc = note_reader(s, cone, st);
-        cone_lock.unlock();
-        if (rc) return rc;
-    }
+    if (cone) cone_lock.unlock();   // enqueued: a recycle now waits for this render
     if (stats) VX_HIP(hipEventRecord(s->ev1, st));
     if (stats) {
         unsigned long long v[ST_COUNT];
