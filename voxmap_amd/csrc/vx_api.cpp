@@ -496,6 +496,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.sunp = s->d_sunp;
     a.sunx = (p->flags & VX_FLAG_NO_EXIT) ? nullptr : s->d_sunx;
     a.SB = s->SB;
+    a.SBf = (float)s->SB;
     a.SXp = s->SXp;
     a.SXpYp = (unsigned)s->SXp * (unsigned)s->SYp;
     a.sunp_texels = (unsigned)s->SXp * (unsigned)s->SYp * (unsigned)s->SZp;

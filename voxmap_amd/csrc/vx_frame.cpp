@@ -81,6 +81,7 @@ void frame_consts(const vx_frame_params &p, int w, int h, int X, int Y, int Z, i
     for (int i = 0; i < 3; i++) {
         fc.cam_cell[i] = p.cam_cell[i];
         fc.cam_fract[i] = p.cam_fract[i];
+        fc.cam_cell_f[i] = (float)p.cam_cell[i];
         fc.fwd[i] = p.ray_fwd[i];
         fc.right[i] = p.ray_right[i];
         fc.up[i] = p.ray_up[i];

@@ -41,6 +41,7 @@ void sun_samples(const float sun[3], float radius, int n, float out[][3]);
 struct FrameConsts {
     int cam_cell[3];
     float cam_fract[3];
+    float cam_cell_f[3];               // (float)cam_cell: exact (|cam_cell| < 2^22, vx_host checks)
     // primary traversal setup, per axis (the kernel's former per-lane fp32 ops):
     // grid slab (float)(0 - cam_cell) - cam_fract, (float)(dim - cam_cell) - cam_fract,
     // and the camera-relative cell range (float)(-cam_cell), (float)(dim - cam_cell - 1)
@@ -74,6 +75,7 @@ struct KernelArgs {
     const uint8_t *sun;      // R channel then G channel, X*Y*Z bytes each
     const int8_t *sunp;      // R then G, int8, inside a border of SB cells of -1 (nullptr: Z > 126)
     int SB;                  // border width of sunp (Z + 2: a march step moves <= Z + 1 cells per axis)
+    float SBf;               // (float)SB
     int SXp;                 // padded row length of sunp
     unsigned SXpYp, sunp_texels;
     const int8_t *sunx;      // 8 orthant-exit copies of sunp's channel, one per ray octant (bit i: r_i > 0), or nullptr

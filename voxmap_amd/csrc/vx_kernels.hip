@@ -144,7 +144,7 @@ struct Surf {            // one G-buffer record (what render.vert hands render.f
     int id;              // 0 block, 1 sky, 2 glass
     int color;           // palette index
     int nidx;            // normal index 0..5 (render.vert:14-17)
-    int c0, c1, c2;      // v_cellPos
+    float c0, c1, c2;    // v_cellPos (exact integers: fp32 keeps the consumers' arithmetic convert-free)
     float f0, f1, f2;    // v_fractPos
 };
 
@@ -341,14 +341,14 @@ __device__ __forceinline__ float march_len_fract(const SunRay &S, float f0, floa
     return len;
 }
 
-__device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
+__device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S, const uint8_t *sun, float c0, float c1, float c2, float f0,
                            float f1, float f2, Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = F.max_steps;
     if (maxs <= 0) return maxs == 0;
     float safe = 1.0f;
-    float e0 = (float)c0, e1 = (float)c1, e2 = (float)c2;
+    float e0 = c0, e1 = c1, e2 = c2;
     float len = march_len(S, f0, f1, f2);
     int step = 0;
     const unsigned nl = active_lanes();
@@ -445,12 +445,12 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
 }
 
 template <int SG>   // the sun's axis signs (bit i: r_i > 0)
-__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, int c0, int c1,
-                                          int c2, float f0, float f1, float f2, Counters &cnt) {
+__device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, float c0, float c1,
+                                          float c2, float f0, float f1, float f2, Counters &cnt) {
     const float xpf = (float)a.SXp;
     constexpr float kBias = 8388608.0f;
-    const float exy = __builtin_fmaf((float)(c1 + a.SB), xpf, (float)(c0 + a.SB) + kBias);
-    const float e2 = (float)(c2 + a.SB) + kBias;
+    const float exy = __builtin_fmaf(c1 + a.SBf, xpf, (c0 + a.SBf) + kBias);   // exact integers
+    const float e2 = (c2 + a.SBf) + kBias;
     const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);   // (pointer arithmetic: keeps the global address space)
     return march_pad_from<SG>(a, S, rsrc, exy, e2, march_len_sg<SG>(S, f0, f1, f2), f0, f1, f2, cnt);
 }
@@ -460,13 +460,13 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
 // descriptor and the first step's fract terms d_i are the same for every
 // sample, so they are formed once; only the three quotients by |r_k| differ.
 template <int SG>
-__device__ __forceinline__ int march_soft(const KernelArgs &a, const int8_t *sun, int c0, int c1, int c2, float f0,
+__device__ __forceinline__ int march_soft(const KernelArgs &a, const int8_t *sun, float c0, float c1, float c2, float f0,
                                           float f1, float f2, Counters &cnt) {
     const FrameConsts &F = a.fc;
     const float xpf = (float)a.SXp;
     constexpr float kBias = 8388608.0f;
-    const float exy = __builtin_fmaf((float)(c1 + a.SB), xpf, (float)(c0 + a.SB) + kBias);
-    const float e2 = (float)(c2 + a.SB) + kBias;
+    const float exy = __builtin_fmaf(c1 + a.SBf, xpf, (c0 + a.SBf) + kBias);
+    const float e2 = (c2 + a.SBf) + kBias;
     const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);
     const float d0 = ((SG & 1) ? ceilf(f0) - f0 : f0 - floorf(f0)) + 1e-4f;     // march_len_sg's terms
     const float d1 = ((SG & 2) ? ceilf(f1) - f1 : f1 - floorf(f1)) + 1e-4f;
@@ -492,7 +492,7 @@ __device__ __forceinline__ int march_soft(const KernelArgs &a, const int8_t *sun
 // three bit patterns is below bits(8.0f) (a negative local has its sign bit set).
 template <int SG>
 __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S, const int8_t *sun,
-                                            const int8_t *brick, int ox, int oy, int oz, int c0, int c1, int c2,
+                                            const int8_t *brick, int ox, int oy, int oz, float c0, float c1, float c2,
                                             float f0, float f1, float f2, Counters &cnt) {
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
     const int maxs = a.fc.max_steps;
@@ -500,7 +500,7 @@ __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S
     constexpr float kBias = 8388608.0f;
     const float xpf = (float)a.SXp;
     const int8_t *sunb = sun - 0x4B000000;
-    float e0 = (float)(c0 + a.SB) + kBias, e1 = (float)(c1 + a.SB), e2 = (float)(c2 + a.SB) + kBias;
+    float e0 = (c0 + a.SBf) + kBias, e1 = c1 + a.SBf, e2 = (c2 + a.SBf) + kBias;
     // brick origin (padded cells, same biases as the cells)
     const float b0 = (float)ox + kBias, b1 = (float)oy, b2 = (float)oz + kBias;
     const unsigned sxpyp = a.SXpYp;
@@ -541,8 +541,9 @@ __device__ __forceinline__ bool march_brick(const KernelArgs &a, const SunRay &S
 
 // Literal path for any other sun direction (zero or tiny components: the
 // 0*inf = NaN and ivec3(floor(NaN)) := 0 rules of the contract apply).
-__device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, int c0, int c1, int c2, float f0,
-                              float f1, float f2, Counters &cnt) {
+__device__ __forceinline__ bool march_literal(const KernelArgs &a, const SunRay &S, const uint8_t *sun, float cf0, float cf1,
+                                              float cf2, float f0, float f1, float f2, Counters &cnt) {
+    int c0 = (int)cf0, c1 = (int)cf1, c2 = (int)cf2;      // exact integers
     const FrameConsts &F = a.fc;
     const float s0 = S.sign[0], s1 = S.sign[1], s2 = S.sign[2];
     const float a0 = S.abs[0], a1 = S.abs[1], a2 = S.abs[2];
@@ -605,8 +606,9 @@ __device__ __forceinline__ bool first_step_exit(const KernelArgs &a, const int8_
     const float fl0 = floorf(g.f0), fl1 = floorf(g.f1), fl2 = floorf(g.f2);
     const float fj = ax == 0 ? g.f1 - fl1 : g.f0 - fl0, fk = ax == 2 ? g.f1 - fl1 : g.f2 - fl2;
     const bool ok = spos != nneg && fj >= 0.0f && fj < 1.0f && fk >= 0.0f && fk < 1.0f;
-    const int x = g.c0 + (ax == 0 ? (nneg ? -1 : 0) : (int)fl0), y = g.c1 + (ax == 1 ? (nneg ? -1 : 0) : (int)fl1),
-              z = g.c2 + (ax == 2 ? (nneg ? -1 : 0) : (int)fl2);
+    const float nb = nneg ? -1.0f : 0.0f;
+    const int x = (int)(g.c0 + (ax == 0 ? nb : fl0)), y = (int)(g.c1 + (ax == 1 ? nb : fl1)),
+              z = (int)(g.c2 + (ax == 2 ? nb : fl2));                 // exact integers
     // the air cell is inside the padded copy (a face lies inside the grid or on its edge)
     const unsigned off = (unsigned)(x + a.SB) + (unsigned)a.SXp * (unsigned)(y + a.SB) + a.SXpYp * (unsigned)(z + a.SB);
     const float v = ok ? ld_fmt1(buf_rsrc(ch, kRsrcS8), off) : 0.0f;
@@ -617,7 +619,7 @@ __device__ __forceinline__ bool first_step_exit(const KernelArgs &a, const int8_
 // S by value: the soft-shadow loop indexes sun_k[k] dynamically, and a
 // reference into the kernel argument there made the compiler copy the whole
 // KernelArgs (1.5 KB) to scratch.
-__device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, int c0, int c1, int c2, float f0,
+__device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, float c0, float c1, float c2, float f0,
                                           float f1, float f2, Counters &cnt) {
     if (S.fast && a.sunp) {
         // wave-uniform switch on the frame's sun signs: one specialised loop each
@@ -848,14 +850,14 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         }
     }
     if (gl) {
-        const int up = gpos ? 0 : 1;
+        const float upf = gpos ? 0.0f : 1.0f;
         const float r0 = gr0 - gq0, r1 = gr1 - gq1, r2 = gr2 - gq2;   // quad origin (exact small integers)
         g0.id = 2;
         g0.color = kGlass;
         g0.nidx = 2 * gax + (gpos ? 1 : 0);
-        g0.c0 = (int)r0 + cc0 + (gax == 0 ? up : 0);
-        g0.c1 = (int)r1 + cc1 + (gax == 1 ? up : 0);
-        g0.c2 = (int)r2 + cc2 + (gax == 2 ? up : 0);
+        g0.c0 = (r0 + F.cam_cell_f[0]) + (gax == 0 ? upf : 0.0f);      // exact integers
+        g0.c1 = (r1 + F.cam_cell_f[1]) + (gax == 1 ? upf : 0.0f);
+        g0.c2 = (r2 + F.cam_cell_f[2]) + (gax == 2 ? upf : 0.0f);
         g0.f0 = gax == 0 ? 0.0f : (o0 + gt * d0) - r0;
         g0.f1 = gax == 1 ? 0.0f : (o1 + gt * d1) - r1;
         g0.f2 = gax == 2 ? 0.0f : (o2 + gt * d2) - r2;
@@ -863,14 +865,14 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     }
     if (hit) {
         Surf &h = gl ? g1 : g0;
-        const int up = hpos ? 0 : 1;
+        const float upf = hpos ? 0.0f : 1.0f;
         const float r0 = hr0 - hq0, r1 = hr1 - hq1, r2 = hr2 - hq2;
         h.id = col == kGlass ? 2 : 0;
         h.color = (int)col;
         h.nidx = 2 * hax + (hpos ? 1 : 0);
-        h.c0 = (int)r0 + cc0 + (hax == 0 ? up : 0);
-        h.c1 = (int)r1 + cc1 + (hax == 1 ? up : 0);
-        h.c2 = (int)r2 + cc2 + (hax == 2 ? up : 0);
+        h.c0 = (r0 + F.cam_cell_f[0]) + (hax == 0 ? upf : 0.0f);
+        h.c1 = (r1 + F.cam_cell_f[1]) + (hax == 1 ? upf : 0.0f);
+        h.c2 = (r2 + F.cam_cell_f[2]) + (hax == 2 ? upf : 0.0f);
         h.f0 = hax == 0 ? 0.0f : (o0 + te * d0) - r0;
         h.f1 = hax == 1 ? 0.0f : (o1 + te * d1) - r1;
         h.f2 = hax == 2 ? 0.0f : (o2 + te * d2) - r2;
@@ -1007,9 +1009,9 @@ __device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float 
     h.id = 2;
     h.color = kGlass;
     h.nidx = 2 * bax + (bst > 0 ? 1 : 0);
-    h.c0 = bx - of0 + cc0 + (bax == 0 ? up : 0);
-    h.c1 = by - of1 + cc1 + (bax == 1 ? up : 0);
-    h.c2 = bz - of2 + cc2 + (bax == 2 ? up : 0);
+    h.c0 = (float)(bx - of0 + cc0 + (bax == 0 ? up : 0));
+    h.c1 = (float)(by - of1 + cc1 + (bax == 1 ? up : 0));
+    h.c2 = (float)(bz - of2 + cc2 + (bax == 2 ? up : 0));
     h.f0 = bax == 0 ? 0.0f : (o0 + bt * d0) - (float)(bx - of0);
     h.f1 = bax == 1 ? 0.0f : (o1 + bt * d1) - (float)(by - of1);
     h.f2 = bax == 2 ? 0.0f : (o2 + bt * d2) - (float)(bz - of2);
@@ -1039,16 +1041,16 @@ __device__ __forceinline__ void lin_axis(float coord, int size, int &i0, int &i1
 // (i <= -1: (0, 0); i >= X - 1: (X - 1, X - 1); else (i, i + 1) -- exactly
 // lin_axis's CLAMP_TO_EDGE pair).  Four 8_8_8_8 UNORM loads per sample
 // instead of eight 8_8 ones, the same RN(b / 255) values, the same lerps.
-__device__ __forceinline__ float sdf_lin(const KernelArgs &a, int c0, int c1, int c2, float f0, float f1, float f2) {
+__device__ __forceinline__ float sdf_lin(const KernelArgs &a, float c0, float c1, float c2, float f0, float f1, float f2) {
     const FrameConsts &F = a.fc;
     int y0, y1, z0, z1;
     float wx, wy, wz;
-    const float ux = ((float)c0 + f0) * F.sf[0] * (float)a.X - 0.5f;
+    const float ux = (c0 + f0) * F.sf[0] * (float)a.X - 0.5f;
     const float flx = floorf(ux);
     wx = ux - flx;
     const int px = min(max((int)flx, -1), a.X - 1) + 1;     // pair index (AO coordinates are far inside +-2^24)
-    lin_axis(((float)c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
-    lin_axis(((float)c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
+    lin_axis((c1 + f1) * F.sf[1], a.Y, y0, y1, wy);
+    lin_axis((c2 + f2) * F.sf[2], a.Z, z0, z1, wz);
     // one byte offset and two deltas (0 or one row / plane: the clamped corners
     // differ by at most one cell per axis)
     const unsigned row = (unsigned)a.X + 1u;
@@ -1240,8 +1242,8 @@ __device__ __forceinline__ float block_shade_factor(const KernelArgs &a, const S
     const float n1 = ni == 2 ? 1.0f : (ni == 3 ? -1.0f : 0.0f);
     const float n2 = ni == 4 ? 1.0f : (ni == 5 ? -1.0f : 0.0f);
     const int ax = ni >> 1;
-    const float u = ax == 0 ? (float)g.c1 + g.f1 : (float)g.c0 + g.f0;
-    const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;
+    const float u = ax == 0 ? g.c1 + g.f1 : g.c0 + g.f0;
+    const float v = ax == 2 ? g.c1 + g.f1 : g.c2 + g.f2;
     float w0, w1, w2, m0, m1, m2;
     white(a, u * kRoughScale, v * kRoughScale, w0, w1, w2);
     normalize3_ranged(n0 + kRoughAmp * w0, n1 + kRoughAmp * w1, n2 + kRoughAmp * w2, m0, m1, m2);
@@ -1263,9 +1265,9 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
     if (EXT && has_ray) {
         r0 = q0; r1 = q1; r2 = q2;
     } else {
-        normalize3((float)(g.c0 - F.cam_cell[0]) + (g.f0 - F.cam_fract[0]),
-                   (float)(g.c1 - F.cam_cell[1]) + (g.f1 - F.cam_fract[1]),
-                   (float)(g.c2 - F.cam_cell[2]) + (g.f2 - F.cam_fract[2]), r0, r1, r2);   // :154
+        normalize3((g.c0 - F.cam_cell_f[0]) + (g.f0 - F.cam_fract[0]),        // exact cell differences
+                   (g.c1 - F.cam_cell_f[1]) + (g.f1 - F.cam_fract[1]),
+                   (g.c2 - F.cam_cell_f[2]) + (g.f2 - F.cam_fract[2]), r0, r1, r2);   // :154
     }
     if (EXT && ray_out) { ray_out[0] = r0; ray_out[1] = r1; ray_out[2] = r2; }
     // shading normal: geometric, or (ext ROUGH) jittered by white() noise
@@ -1274,8 +1276,8 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
     if (rough) {
         cnt.rough++;
         const int ax = ni >> 1;
-        const float u = ax == 0 ? (float)g.c1 + g.f1 : (float)g.c0 + g.f0;   // first in-face axis
-        const float v = ax == 2 ? (float)g.c1 + g.f1 : (float)g.c2 + g.f2;   // second
+        const float u = ax == 0 ? g.c1 + g.f1 : g.c0 + g.f0;   // first in-face axis
+        const float v = ax == 2 ? g.c1 + g.f1 : g.c2 + g.f2;   // second
         float w0, w1, w2;
         white(a, u * kRoughScale, v * kRoughScale, w0, w1, w2);
         // |n + 0.1 w| lies in [0.89, 1.11] (unit axis n, |w_i| <= 1): rcp_ranged is exact
@@ -1286,7 +1288,7 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
     float amb0 = 1.0f, amb1 = 1.0f, amb2 = 1.0f;
     if (!(F.flags & VX_FLAG_NO_AO)) {                                                  // :223-225
         cnt.ao++;
-        const float ambDist = sdf_lin(a, g.c0 + (int)n0, g.c1 + (int)n1, g.c2 + (int)n2, g.f0, g.f1, g.f2);
+        const float ambDist = sdf_lin(a, g.c0 + n0, g.c1 + n1, g.c2 + n2, g.f0, g.f1, g.f2);
         const float ambFactor = gmin(1.0f - sqrtf(ambDist), 0.8f);
         amb0 = gmix(1.0f, F.shadeCol[0], ambFactor);
         amb1 = gmix(1.0f, F.shadeCol[1], ambFactor);
@@ -1410,9 +1412,9 @@ __device__ __forceinline__ int walk_reflect(const KernelArgs &a, int B0, int B1,
             h.color = col;
             h.id = col == kGlass ? 2 : 0;
             h.nidx = 2 * ax + (stp > 0 ? 1 : 0);
-            h.c0 = x + (ax == 0 && stp < 0 ? 1 : 0);
-            h.c1 = y + (ax == 1 && stp < 0 ? 1 : 0);
-            h.c2 = z + (ax == 2 && stp < 0 ? 1 : 0);
+            h.c0 = (float)(x + (ax == 0 && stp < 0 ? 1 : 0));
+            h.c1 = (float)(y + (ax == 1 && stp < 0 ? 1 : 0));
+            h.c2 = (float)(z + (ax == 2 && stp < 0 ? 1 : 0));
             h.f0 = ax == 0 ? 0.0f : (o0 + te * d0) - (float)c0;
             h.f1 = ax == 1 ? 0.0f : (o1 + te * d1) - (float)c1;
             h.f2 = ax == 2 ? 0.0f : (o2 + te * d2) - (float)c2;
@@ -1433,9 +1435,9 @@ __device__ __forceinline__ void reflect_color(const KernelArgs &a, const Surf &g
     const int ax = gl.nidx >> 1;
     const float R0 = ax == 0 ? -rd[0] : rd[0], R1 = ax == 1 ? -rd[1] : rd[1], R2 = ax == 2 ? -rd[2] : rd[2];
     const float fl0 = floorf(gl.f0), fl1 = floorf(gl.f1), fl2 = floorf(gl.f2);
-    const int B0 = ax == 0 ? gl.c0 : gl.c0 + f2i(fl0);
-    const int B1 = ax == 1 ? gl.c1 : gl.c1 + f2i(fl1);
-    const int B2 = ax == 2 ? gl.c2 : gl.c2 + f2i(fl2);
+    const int B0 = (int)(ax == 0 ? gl.c0 : gl.c0 + fl0);                // exact integers
+    const int B1 = (int)(ax == 1 ? gl.c1 : gl.c1 + fl1);
+    const int B2 = (int)(ax == 2 ? gl.c2 : gl.c2 + fl2);
     const float o0 = ax == 0 ? 0.0f : gl.f0 - fl0;
     const float o1 = ax == 1 ? 0.0f : gl.f1 - fl1;
     const float o2 = ax == 2 ? 0.0f : gl.f2 - fl2;
@@ -1603,7 +1605,7 @@ void k_render(KernelArgs a) {
     // the compacted marching fragments' start (fract, cell) and lit counts
     __shared__ float4 s_sunk[kPool ? 3 * VX_MAX_SHADOW_SAMPLES : 1];
     __shared__ float4 s_pf[kPool ? kWG : 1];
-    __shared__ int4 s_pc[kPool ? kWG : 1];
+    __shared__ float4 s_pc[kPool ? kWG : 1];
     __shared__ int s_plit[kPool ? kWG : 1];
     __shared__ int s_brick[kBrick ? 4 * 4 * 128 : 1];      // per wave: 4 bricks of 8x8x8 int8 (dwords)
     if (kPool) {
@@ -1686,7 +1688,7 @@ void k_render(KernelArgs a) {
                 const int slot = __popcll(mask & ((1ull << lane) - 1ull));
                 if (need) {
                     s_pf[wb + slot] = make_float4(g[0].f0, g[0].f1, g[0].f2, 0.0f);
-                    s_pc[wb + slot] = make_int4(g[0].c0, g[0].c1, g[0].c2, 0);
+                    s_pc[wb + slot] = make_float4(g[0].c0, g[0].c1, g[0].c2, 0.0f);
                     s_plit[wb + slot] = 0;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1718,10 +1720,10 @@ void k_render(KernelArgs a) {
                         for (int j = 0; j < 8; j++) {
                             const int d = lane + 64 * j, bi = d >> 7, row = (d & 127) >> 1, half = d & 1;
                             const int fb = min(base + bi, nf - 1);
-                            const int4 pc = s_pc[wb + fb];
+                            const float4 pc = s_pc[wb + fb];
                             const float4 pf = s_pf[wb + fb];     // anchor: the start's unit cell c + floor(f)
-                            const int ox = (pc.x + (int)floorf(pf.x) + a.SB - bx) & ~3,
-                                      oy = pc.y + (int)floorf(pf.y) + a.SB - by, oz = pc.z + (int)floorf(pf.z) + a.SB - bz;
+                            const int ox = ((int)(pc.x + floorf(pf.x)) + a.SB - bx) & ~3,
+                                      oy = (int)(pc.y + floorf(pf.y)) + a.SB - by, oz = (int)(pc.z + floorf(pf.z)) + a.SB - bz;
                             const size_t off = (size_t)(unsigned)ox + 4u * half +
                                                (size_t)(unsigned)a.SXp * (unsigned)(oy + (row & 7)) +
                                                (size_t)a.SXpYp * (unsigned)(oz + (row >> 3));
@@ -1732,14 +1734,14 @@ void k_render(KernelArgs a) {
                     }
                     if (klane && fs < nf) {
                         const float4 pf = s_pf[wb + fs];
-                        const int4 pc = s_pc[wb + fs];
+                        const float4 pc = s_pc[wb + fs];
                         cnt.shadow_rays++;
                         bool lit;
                         if constexpr (kBrick) {
                             const int8_t *br = reinterpret_cast<const int8_t *>(s_brick + (wb >> 6) * 512) +
                                                512 * (lane >> lg);
-                            const int ox = (pc.x + (int)floorf(pf.x) + a.SB - bx) & ~3,
-                                      oy = pc.y + (int)floorf(pf.y) + a.SB - by, oz = pc.z + (int)floorf(pf.z) + a.SB - bz;
+                            const int ox = ((int)(pc.x + floorf(pf.x)) + a.SB - bx) & ~3,
+                                      oy = (int)(pc.y + floorf(pf.y)) + a.SB - by, oz = (int)(pc.z + floorf(pf.z)) + a.SB - bz;
                             switch (sgv) {
 #define VX_SGB(K) case K: lit = march_brick<K>(a, S, ch, br, ox, oy, oz, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
                                                cnt); break;
