@@ -27,8 +27,10 @@ def test_render_kernels_fit_eight_waves_and_no_arg_copy(meta):
     for p, v in _render(meta).items():
         lim = kernel_meta.STATS_SCRATCH_LIMIT if p[1] else kernel_meta.RENDER_SCRATCH_LIMIT
         assert v["private_segment_fixed_size"] <= lim, (p, v)
-        if not p[1] and p[3] != 4:                     # timed (non-STATS) kernels
+        if not p[1] and p[3] < 4:                      # timed (non-STATS) kernels
             assert v["vgpr_count"] <= 64 and v["sgpr_count"] <= 80, (p, v)
+        elif not p[1] and p[3] >= 5:                   # EXT 5/6: their own budget (VX_GEN_ATTR)
+            assert v["vgpr_count"] <= kernel_meta.GENERAL_VGPR_LIMIT, (p, v)
         elif not p[1]:                                 # EXT 4: LDS bricks hold it to 7 waves/SIMD anyway
             assert v["vgpr_count"] <= 80, (p, v)
 

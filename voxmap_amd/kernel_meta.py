@@ -26,6 +26,7 @@ STATS_SCRATCH_LIMIT = 512       # the counting (STATS) instantiations keep ~16 c
 # (0 v1, 1 extensions, 2 soft shadows, 3 pooled, 4 LDS bricks, 5/6 glass in draw order)
 SPILL_LIMITS = {0: 0, 1: 0, 2: 4, 3: 4, 4: 40}
 RENDER_VGPR_LIMIT = 64          # 8 waves/SIMD
+GENERAL_VGPR_LIMIT = 80         # EXT 5/6: 6 waves/SIMD (VX_GEN_ATTR)
 
 
 def _tool(name: str) -> str:
@@ -69,7 +70,7 @@ def kernels(lib: str) -> dict[str, dict[str, int]]:
 
 def render_params(name: str):
     """(FMT, STATS, TILED, EXT, F32IDX) of a mangled k_render instantiation, else None."""
-    m = re.search(r"k_renderILi(\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)E", name)
+    m = re.search(r"k_render(?:_gen)?ILi(\d)ELb(\d)ELb(\d)ELi(\d)ELb(\d)E", name)
     return tuple(int(g) for g in m.groups()) if m else None
 
 
@@ -94,7 +95,9 @@ def check(lib: str) -> dict[str, dict[str, int]]:
         spill_lim = SPILL_LIMITS.get(p[3]) if p is not None and not stats else None
         if spill_lim is not None and v.get("vgpr_spill_count", 0) > spill_lim:
             bad.append(f"{name}: {v['vgpr_spill_count']} VGPRs spilled > {spill_lim}")
-        if not stats and v.get("vgpr_count", 0) > (80 if brick else RENDER_VGPR_LIMIT):
+        # EXT 5/6 (glass in draw order, REFLECT_ALL): a budget of their own (VX_GEN_ATTR, 6 waves/SIMD)
+        general = p is not None and p[3] >= 5
+        if not stats and v.get("vgpr_count", 0) > (80 if brick else GENERAL_VGPR_LIMIT if general else RENDER_VGPR_LIMIT):
             bad.append(f"{name}: {v['vgpr_count']} VGPRs > {RENDER_VGPR_LIMIT}")
     if bad:
         raise RuntimeError("render kernel resource check failed:\n  " + "\n  ".join(bad))
