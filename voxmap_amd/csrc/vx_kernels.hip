@@ -1592,7 +1592,8 @@ static_assert(kBX == 1 << kBXS && kBY == 1 << kBYS, "block shape");
 // inlined primary() copies in one kernel make the compiler copy KernelArgs
 // to scratch.
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
-__device__ __forceinline__ void render_block(const KernelArgs &a) {
+__global__ __launch_bounds__(kWG) VX_OCC_ATTR
+void k_render(KernelArgs a) {
     // the shading instantiation: EXT 3/4 shade as 2; 5/6 are 1/2 with the general
     // shading block (glass in draw order, REFLECT_ALL)
     constexpr int XE = EXT == 5 ? 1 : (EXT >= 2 ? 2 : EXT);
@@ -1913,27 +1914,6 @@ if constexpr (!kGeneral) {
     }
 }
 
-// The timed kernels: EXT 0-4 at 8 waves/SIMD (VX_OCC_ATTR).  EXT 5/6 (glass in
-// draw order, REFLECT_ALL: the general shading loop) hold a pane's record, the
-// walk state and the mirror walk live at once; at the 80-SGPR / 64-VGPR budget
-// they spilled inside the march and walk loops (v_readlane/v_writelane every
-// step), so they get a budget of their own (VX_GEN_ATTR).
-#ifndef VX_GEN_ATTR
-#define VX_GEN_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
-#endif
-template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
-__global__ __launch_bounds__(kWG) VX_OCC_ATTR
-void k_render(KernelArgs a) {
-    static_assert(EXT < 5, "EXT 5/6: k_render_gen");
-    render_block<FMT, STATS, TILED, EXT, F32IDX>(a);
-}
-template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
-__global__ __launch_bounds__(kWG) VX_GEN_ATTR
-void k_render_gen(KernelArgs a) {
-    static_assert(EXT >= 5, "EXT 0-4: k_render");
-    render_block<FMT, STATS, TILED, EXT, F32IDX>(a);
-}
-
 // 2D mode frames (quality 0) in a kernel of their own: the 3D kernel keeps its
 // code and registers (a third user of the frame constants in k_render made
 // the compiler copy KernelArgs to scratch).  Same pixel mapping and stores.
@@ -2056,7 +2036,7 @@ __global__ void k_reduce_stats(unsigned long long *stats) {
 template <int F, bool S, bool T, int E>
 static void launch_k(const KernelArgs &a, dim3 grid, dim3 block, hipStream_t s) {
     if constexpr (E >= 5) {           // glass in draw order: the integer primary index only
-        hipLaunchKernelGGL((k_render_gen<F, S, T, E, false>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, block, 0, s, a);
     } else {
         if (a.prim_f32)
             hipLaunchKernelGGL((k_render<F, S, T, E, true>), grid, block, 0, s, a);

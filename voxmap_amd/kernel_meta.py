@@ -26,7 +26,7 @@ STATS_SCRATCH_LIMIT = 512       # the counting (STATS) instantiations keep ~16 c
 # (0 v1, 1 extensions, 2 soft shadows, 3 pooled, 4 LDS bricks, 5/6 glass in draw order)
 SPILL_LIMITS = {0: 0, 1: 0, 2: 4, 3: 4, 4: 40}
 RENDER_VGPR_LIMIT = 64          # 8 waves/SIMD
-GENERAL_VGPR_LIMIT = 80         # EXT 5/6: 6 waves/SIMD (VX_GEN_ATTR)
+GENERAL_VGPR_LIMIT = 96         # EXT 5/6: 5 waves/SIMD (VX_GEN_ATTR)
 
 
 def _tool(name: str) -> str:
