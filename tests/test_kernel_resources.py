@@ -29,7 +29,7 @@ def test_render_kernels_fit_eight_waves_and_no_arg_copy(meta):
         assert v["private_segment_fixed_size"] <= lim, (p, v)
         if not p[1] and p[3] < 4:                      # timed (non-STATS) kernels
             assert v["vgpr_count"] <= 64 and v["sgpr_count"] <= 80, (p, v)
-        elif not p[1] and p[3] >= 5:                   # EXT 5/6: their own budget (VX_GEN_ATTR)
+        elif not p[1] and p[3] >= 5:                   # EXT 5/6: their own budget (vx_render_e56.hip)
             assert v["vgpr_count"] <= kernel_meta.GENERAL_VGPR_LIMIT, (p, v)
         elif not p[1]:                                 # EXT 4: LDS bricks hold it to 7 waves/SIMD anyway
             assert v["vgpr_count"] <= 80, (p, v)

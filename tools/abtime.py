@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--flags", default="0,48")
     ap.add_argument("--samples", type=int, default=None)
+    ap.add_argument("--scene", default=None, help="override the config's scene (e.g. s_glass)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("variants", nargs="+")
@@ -33,7 +34,7 @@ def main():
     from voxmap_amd import _abi, presets
     torch.cuda.set_device(0)
     cfg = presets.CONFIGS[args.config]
-    grid = presets.scene_grid(cfg["scene"])
+    grid = presets.scene_grid(args.scene or cfg["scene"])
     Z, Y, X = grid.shape
     W, H = cfg["w"], cfg["h"]
     up = 3.0 if cfg["scene"] == "s_up3" else 1.0

@@ -14,8 +14,12 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libvoxmap_hip.so")
-SOURCES = ["vx_api.cpp", "vx_host.cpp", "vx_codec.cpp", "vx_field.cpp", "vx_frame.cpp", "vx_mgpu.cpp", "vx_kernels.hip",
-           "vx_field_gpu.hip"]
+# the render kernel's EXT modes compile in units of their own (vx_render.h), listed
+# first: they are the long ones, and the pool starts them first
+SOURCES = ["vx_render_e56.hip", "vx_render_e2.hip", "vx_render_e1.hip", "vx_render_e0.hip", "vx_render_e3.hip",
+           "vx_render_e4.hip", "vx_kernels.hip", "vx_field_gpu.hip", "vx_api.cpp", "vx_host.cpp", "vx_codec.cpp",
+           "vx_field.cpp", "vx_frame.cpp", "vx_mgpu.cpp"]
+HEADERS = ["vx_internal.h", "vx_render.h"]
 ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
 # -fno-slp-vectorize: packed FP32 (v_pk_*) issues at the cost of two scalar ops
 # on gfx950 (profiles/r01_valu_costs.txt), so SLP packing only adds moves.
@@ -53,8 +57,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [
-        os.path.join(CSRC, "vx_internal.h"), os.path.join(HERE, "..", "include", "voxmap.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(HERE, "..", "include", "voxmap.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
@@ -71,7 +74,7 @@ def build(force: bool = False, verbose: bool = True, out: str | None = None, def
     os.makedirs(objdir, exist_ok=True)
     flags = [*FLAGS, *extra_flags, *[f"-D{d}" for d in defines]]
     jobs, objs = [], []
-    hdrs = [os.path.join(CSRC, "vx_internal.h"), os.path.join(HERE, "..", "include", "voxmap.h"), __file__]
+    hdrs = [*(os.path.join(CSRC, h) for h in HEADERS), os.path.join(HERE, "..", "include", "voxmap.h"), __file__]
     for src in SOURCES:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
