@@ -45,7 +45,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-BAND = 64               # rows per band of the multi-GPU deal
 
 
 def parse(argv=None):
@@ -319,6 +318,8 @@ def lane_utils(s):
 # ---------------------------------------------------------------- N > 1
 def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local, standin):
     """Bands dealt round-robin, rendered in place, gathered to rank 0; timed max over ranks."""
+    from voxmap_amd.dist import band_rows_for, rows_per_rank
+    BAND = band_rows_for(H, world)      # the band height whose deal loads the busiest rank least
     dev = "cpu" if standin else "cuda"
     sync = (lambda: None) if standin else torch.cuda.synchronize
     mg = split_ms = None
@@ -443,7 +444,9 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
         except Exception as e:            # never let the diagnostic break the bench line
             split_ms = {"error": str(e)}
         mg.close()
+    rpr = rows_per_rank(H, BAND, world)
     shards = {"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
+              "rows_per_rank_max_over_mean": round(max(rpr) / (sum(rpr) / world), 5),
               "assignment": "round-robin (band b -> rank b % N)", "gather": gather_desc, "split_ms": split_ms}
     return stats, wall, settle_steps, shards, blocks
 

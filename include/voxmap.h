@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 8
+#define VX_ABI_VERSION 9
 
 /* error codes */
 #define VX_OK 0
@@ -102,14 +102,20 @@ extern "C" {
  * flag v_cellPos is the hit cell and v_fractPos the hit's fraction in it: the
  * same point, another fp32 split. */
 #define VX_FLAG_UNIT_GBUF 0x800u
-/* Glass in draw order (ABI 8): every front-facing glass face in
- * front of the opaque surface is blended as the reference's raster does --
- * glass quads after all opaque ones, in vertex.bin order (sdf.cpp:284,337),
- * depth test LESS with depth writes on, SRC_ALPHA blending (render.js:82-91) --
- * instead of the single layer (the nearest pane over the surface behind it).
- * The nearest VX_MAX_GLASS_LAYERS panes of a pixel take part. */
+/* Glass (ABI 9; DESIGN.md §5 "Glass").  By default every front-facing glass
+ * face in front of the opaque surface is blended as the reference's raster
+ * does: glass quads after all opaque ones, in vertex.bin order (sdf.cpp:284,
+ * 337), depth test LESS with depth writes on, SRC_ALPHA blending
+ * (render.js:82-91) -- a pane is blended iff it is nearer than the last surface
+ * written when its quad is drawn.  The render kernel shades a pixel whose ray
+ * crosses one pane with one blend (the draw order's result) and re-walks the
+ * panes in key order only where two or more stack.
+ * VX_FLAG_GLASS_ORDER: the whole frame through the general draw-order kernel
+ * (diagnostic / A-B: identical frames).  VX_FLAG_GLASS_SINGLE: the nearest
+ * pane only, over the surface behind it (the single layer of ABI <= 8;
+ * diagnostic, differs where panes stack). */
 #define VX_FLAG_GLASS_ORDER 0x1000u
-#define VX_MAX_GLASS_LAYERS 8
+#define VX_FLAG_GLASS_SINGLE 0x8000u
 /* Extension (ABI 8): every first surface mirrors the traced scene, as
  * VX_FLAG_REFLECT does for glass: the surface a pixel shows first (and every
  * pane blended in draw order) adds Schlick F * the colour along its mirror ray
@@ -297,6 +303,11 @@ int vx_mgpu_rank(const vx_mgpu *m, int *nranks, int *rank);
 void vx_mgpu_destroy(vx_mgpu *m);
 /* The deal: the band ids of `rank` (ascending) into ids[0..cap); returns their count. */
 int vx_mgpu_bands(int h, int band_rows, int nranks, int rank, int *ids, int cap);
+/* ABI 9: the band_rows for an h-row frame over nranks ranks -- the multiple of 8
+ * up to max_rows (<= 0: 64) whose deal gives the busiest rank the fewest rows,
+ * ties to the tallest band (a pure host function).  C4 (4320 rows) over 8 GPUs:
+ * 32, i.e. 544 rows for the busiest rank against a mean of 540. */
+int vx_mgpu_band_rows(int h, int nranks, int max_rows);
 /* One point-to-point move of the gather (ABI 6): band `band` (rows
  * [band*band_rows, band*band_rows + rows)) goes from rank `src` (its owner) to
  * rank `dst` = 0; the bytes lie at `offset` of the w x h frame on both ranks. */

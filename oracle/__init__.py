@@ -138,7 +138,7 @@ class Oracle:
             mode = 2 if exit == "orthant" else 1
         self.sc = OScene(X, Y, Z, self.field.ctypes.data, self.noise.ctypes.data, W, H,
                          (C.c_void_p * 8)(*[e.ctypes.data for e in self.oct_e]), self.fp2d.ctypes.data, mode)
-        # the quad table serves the split and the glass draw order (VX_FLAG_GLASS_ORDER)
+        # the quad table serves the split and the glass draw order (its face keys)
         self.qoff = (np.ascontiguousarray(quad, np.uint16) if isinstance(quad, np.ndarray)
                      else face_quads(self.field, chunk))
         assert self.qoff.shape == (Z, Y, X, 6)

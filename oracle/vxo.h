@@ -78,16 +78,18 @@ typedef struct {
 #define VXO_FLAG_REFLECT 0x10u  /* glass reflects the traced scene (README.md:15-20) */
 #define VXO_FLAG_ROUGH 0x20u    /* per-fragment normal jitter from white() (README.md:22, render.frag:21) */
 #define VXO_MAX_SAMPLES 16
-/* Glass in draw order: every front-facing glass face in front of
- * the opaque surface is blended as the reference's raster does -- glass quads
- * drawn after all opaque ones in vertex.bin order (sdf.cpp:284,337), depth test
- * LESS with depth writes on, SRC_ALPHA blending (render.js:82-91) -- instead of
- * the single layer.  Needs the quad table (vxo_scene.qoff).  Up to
- * VXO_MAX_GLASS glass faces per pixel (the nearest ones) are blended. */
+/* Glass (DESIGN.md §5 "Glass"), include/voxmap.h VX_FLAG_GLASS_*: by default
+ * every front-facing glass face in front of the opaque surface is blended as
+ * the reference's raster does -- glass quads drawn after all opaque ones in
+ * vertex.bin order (sdf.cpp:284,337), depth test LESS with depth writes on,
+ * SRC_ALPHA blending (render.js:82-91); every pane the ray crosses takes part.
+ * VXO_FLAG_GLASS_SINGLE: the nearest pane only, over the surface behind it
+ * (diagnostic).  VXO_FLAG_GLASS_ORDER selects the kernel's whole-frame path
+ * and changes nothing here. */
 #define VXO_FLAG_GLASS_ORDER 0x1000u
+#define VXO_FLAG_GLASS_SINGLE 0x8000u
 #define VXO_FLAG_UNIT_GBUF 0x800u   /* the unit-cell G-buffer split (include/voxmap.h VX_FLAG_UNIT_GBUF) */
 #define VXO_FLAG_REFLECT_ALL 0x2000u /* ext: the first surface of every pixel mirrors the scene (as REFLECT glass) */
-#define VXO_MAX_GLASS 8
 
 typedef struct {
     uint64_t pixels, sky_px, block_px, glass_px;

@@ -317,14 +317,27 @@ static inline int in_grid(const vxo_scene *s, const int a[3]) {
     return a[0] >= 0 && a[1] >= 0 && a[2] >= 0 && a[0] < s->X && a[1] < s->Y && a[2] < s->Z;
 }
 
+/* The pane a draw-order scan looks for (glass_layer 3): the front-facing glass
+ * face with the smallest draw key above klast (any key if !have_last) among
+ * those nearer than tmax. */
+typedef struct {
+    int have_last;
+    uint64_t klast;
+    float tmax;
+} glass_sel;
+
 /* Octant-box walk of the ray B + o + t*d (B an integer cell, camera- or
  * origin-relative cells c) from the start cell B + c to the first colour
  * change: from cell c the box [c, c + e*s] (vxo_field_box extents of the ray
- * octant) is all air, so the ray jumps to where it leaves the box.  glass_layer != 0: a glass entry is recorded and the walk goes on to
- * the next change behind it (primary visibility); 0: the first change ends
- * the walk (reflection rays).  A start cell outside the grid is sky. */
+ * octant) is all air, so the ray jumps to where it leaves the box.
+ * glass_layer 1: the first glass entry is recorded and the walk goes on to
+ * the next change behind it (primary visibility); 0: the first change ends the
+ * walk (reflection rays); 3: a draw-order scan (sel): every glass entry before
+ * the first opaque one is a candidate, the one sel picks is g[0], and the
+ * return is 1 if there is one.  A start cell outside the grid is sky. */
 static int walk(const vxo_scene *s, const int cc[3], const float o[3], const float d[3], int c[3],
-                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit, int *glass_entries, int quad) {
+                int glass_layer, vxo_gbuf g[2], int *fetches, int *cap_hit, int *glass_entries, int quad,
+                const glass_sel *sel) {
     const int dims[3] = {s->X, s->Y, s->Z};
     float inv[3];
     int stp[3];
@@ -364,7 +377,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
             }
         }
         abs_c[0] = c[0] + cc[0]; abs_c[1] = c[1] + cc[1]; abs_c[2] = c[2] + cc[2];
-        if (!in_grid(s, abs_c)) return nrec;   /* left the grid: sky behind */
+        if (!in_grid(s, abs_c)) return nrec;   /* left the grid: sky behind (scan: the pane found, if any) */
         tx = texel(s, abs_c[0], abs_c[1], abs_c[2]);
         (*fetches)++;
         const int col = vxo_vis(tx[2]);
@@ -373,11 +386,11 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
         /* a front face: entering a meshed cell from a cell of another colour
          * (air is never meshed, sdf.cpp:229-233,284); glass_layer 1: the
          * first glass entry is recorded and the walk goes on, later glass
-         * entries are not surfaces (one blend layer); 2: every
-         * glass entry is recorded (up to VXO_MAX_GLASS, draw-order blending) */
-        if (col != prev && col != 0 && !(glass_layer == 1 && col == GLASS_INDEX && nrec == 1) &&
-            !(glass_layer == 2 && col == GLASS_INDEX && nrec >= VXO_MAX_GLASS)) {
-            vxo_gbuf *h = &g[nrec];
+         * entries are passed (render_pixel blends them in draw order) */
+        if (glass_layer == 3 && col != prev && col != 0 && col != GLASS_INDEX) return nrec;
+        if (col != prev && col != 0 && !(glass_layer == 1 && col == GLASS_INDEX && nrec == 1)) {
+            vxo_gbuf cand;
+            vxo_gbuf *h = glass_layer == 3 ? &cand : &g[nrec];
             h->color = col;
             h->id = col == GLASS_INDEX ? 2 : 0;
             h->normal_idx = 2 * a + (stp[a] > 0 ? 1 : 0);
@@ -405,8 +418,15 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
                     h->fract[i] = p - (float)(c[i] - off[i]);
                 }
             }
-            nrec++;
-            if (!glass_layer || h->id != 2) return nrec;
+            if (glass_layer == 3) {
+                if ((!sel->have_last || h->key > sel->klast) && h->t < sel->tmax && (!nrec || h->key < g[0].key)) {
+                    g[0] = cand;
+                    nrec = 1;
+                }
+            } else {
+                nrec++;
+                if (!glass_layer || h->id != 2) return nrec;
+            }
         }
         prev = col;
     }
@@ -416,7 +436,7 @@ static int walk(const vxo_scene *s, const int cc[3], const float o[3], const flo
 }
 
 static int primary_walk(const vxo_scene *s, const vxo_frame *f, const float d[3], int glass_layer, vxo_gbuf *g,
-                        int *fetches, int *cap_hit) {
+                        int *fetches, int *cap_hit, int *glass_entries, const glass_sel *sel) {
     const int dims[3] = {s->X, s->Y, s->Z};
     const float *o = f->cam_fract;
     const int *cc = f->cam_cell;
@@ -446,12 +466,12 @@ static int primary_walk(const vxo_scene *s, const vxo_frame *f, const float d[3]
         c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
     }
     const int quad = !s->unit_split && !(f->flags & VXO_FLAG_UNIT_GBUF);
-    return walk(s, cc, o, d, c, glass_layer, g, fetches, cap_hit, NULL, quad);
+    return walk(s, cc, o, d, c, glass_layer, g, fetches, cap_hit, glass_entries, quad, sel);
 }
 
 int vxo_primary(const vxo_scene *s, const vxo_frame *f, const float d[3],
                 vxo_gbuf g[2], int *fetches, int *cap_hit) {
-    return primary_walk(s, f, d, 1, g, fetches, cap_hit);
+    return primary_walk(s, f, d, 1, g, fetches, cap_hit, NULL, NULL);
 }
 
 /* Diagnostic (the single-layer glass deviation): per pixel, the
@@ -492,7 +512,7 @@ void vxo_glass_layers(const vxo_scene *s, const vxo_frame *f, int w, int h, uint
                     c[i] = ci < lo ? lo : (ci > hi ? hi : ci);
                 }
                 vxo_gbuf g[2];       /* (the grid boundary has no faces: a glass start cell is no entry) */
-                walk(s, cc, o, d, c, 1, g, &fetches, &cap, &n, 0);
+                walk(s, cc, o, d, c, 1, g, &fetches, &cap, &n, 0, NULL);
             }
             out[(size_t)py * w + px] = (uint8_t)(n > 255 ? 255 : n);
         }
@@ -832,7 +852,7 @@ static void reflect_color(const shade_ctx *c, const vxo_gbuf *gl, const float rd
     }
     vxo_gbuf h[2];
     int fetches = 0, cap_hit = 0;
-    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit, NULL, 0);
+    const int n = walk(c->s, B, o, R, c0, 0, h, &fetches, &cap_hit, NULL, 0, NULL);
     if (st) { st->reflect_rays++; st->reflect_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
     float rgba[4];
     if (n == 0) {
@@ -931,10 +951,9 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
         shade_2d(c, d, out, st);
         return;
     }
-    vxo_gbuf g[VXO_MAX_GLASS + 1];
-    int fetches = 0, cap_hit = 0;
-    const int order = (f->flags & VXO_FLAG_GLASS_ORDER) && s->qoff;
-    int n = primary_walk(s, f, d, order ? 2 : 1, g, &fetches, &cap_hit);
+    vxo_gbuf g[2];
+    int fetches = 0, cap_hit = 0, panes = 0;
+    int n = primary_walk(s, f, d, 1, g, &fetches, &cap_hit, &panes, NULL);
     if (st) { st->pixels++; st->primary_fetches += (uint64_t)fetches; st->primary_cap_hits += (uint64_t)cap_hit; }
     vxo_gbuf sky;
     sky_record(&sky);
@@ -947,40 +966,40 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
     if (n == 0) {
         if (st) st->sky_px++;
         shade_frag(c, &sky, d, out, NULL, st);
-    } else if (order && g[0].id == 2) {
-        /* the reference's raster: glass quads after every opaque one, in
-         * vertex.bin order; each passes the depth test (LESS, depth writes on)
-         * iff it is nearer than the last surface written, and blends over the
-         * colour there (render.js:82-91) */
+    } else if (panes >= 2 && !(f->flags & VXO_FLAG_GLASS_SINGLE)) {
+        /* two or more panes in front of the surface: the reference's raster --
+         * glass quads after every opaque one, in vertex.bin order; each passes
+         * the depth test (LESS, depth writes on) iff it is nearer than the last
+         * surface written, and blends over the colour there (render.js:82-91).
+         * The next pane drawn is found by a scan of the ray's panes (walk mode 3,
+         * no fetches counted: they repeat the primary walk's).  With one pane
+         * this is the single blend below. */
         if (st) st->glass_px++;
-        int ng = 0;
-        while (ng < n && g[ng].id == 2) ng++;
         float dst[4], depth = INFINITY;
         g_term_slot = 1;
-        if (ng < n) {
-            shade_frag(c, &g[ng], NULL, dst, NULL, st);
-            depth = g[ng].t;
+        if (n == 2) {
+            shade_frag(c, &g[1], NULL, dst, NULL, st);
+            depth = g[1].t;
         } else {
             shade_frag(c, &sky, d, dst, NULL, st);
         }
         g_term_slot = -1;
-        int idx[VXO_MAX_GLASS];
-        for (int k = 0; k < ng; k++) idx[k] = k;
-        for (int k = 1; k < ng; k++)          /* draw order (keys of distinct faces differ) */
-            for (int j = k; j > 0 && g[idx[j]].key < g[idx[j - 1]].key; j--) {
-                const int tmp = idx[j]; idx[j] = idx[j - 1]; idx[j - 1] = tmp;
-            }
-        for (int k = 0; k < ng; k++) {
-            const vxo_gbuf *gl = &g[idx[k]];
-            if (!(gl->t < depth)) continue;   /* behind the last surface written: fails LESS */
+        glass_sel sel = {0, 0, depth};
+        for (;;) {
+            vxo_gbuf gl;
+            int fx = 0, cx = 0;
+            sel.tmax = depth;
+            if (!primary_walk(s, f, d, 3, &gl, &fx, &cx, NULL, &sel)) break;
             float src[4], rd[3];
-            g_term_slot = idx[k] == 0 ? 0 : -1;
-            shade_frag(c, gl, NULL, src, rd, st);
+            g_term_slot = gl.key == g[0].key ? 0 : -1;
+            shade_frag(c, &gl, NULL, src, rd, st);
             g_term_slot = -1;
-            if (f->flags & (VXO_FLAG_REFLECT | VXO_FLAG_REFLECT_ALL)) add_reflection(c, gl, rd, src, st);
+            if (f->flags & (VXO_FLAG_REFLECT | VXO_FLAG_REFLECT_ALL)) add_reflection(c, &gl, rd, src, st);
             const float a = src[3];
             for (int i = 0; i < 3; i++) dst[i] = src[i] * a + dst[i] * (1.0f - a);
-            depth = gl->t;
+            depth = gl.t;
+            sel.have_last = 1;
+            sel.klast = gl.key;
         }
         out[0] = dst[0]; out[1] = dst[1]; out[2] = dst[2];
     } else if (g[0].id != 2) {

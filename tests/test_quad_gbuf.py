@@ -164,8 +164,8 @@ def test_glass_order_two_panes(O, noise, yaw, both):
     Ob = O.Oracle(f, noise, quad=O.face_quads(f))
     # orbit camera (map.js:373-380): position = sbj + Rz(yaw) Rx(rx) (0, 0, sbj.z)
     x = 25.3 - 5.4 if both else 6.3 + 5.4
-    fr = vx.make_frame((x, 12.2, 5.4), (1.5707, 0.0, yaw), 32, 32)
-    fo = vx.make_frame((x, 12.2, 5.4), (1.5707, 0.0, yaw), 32, 32, flags=0x1000)
+    fr = vx.make_frame((x, 12.2, 5.4), (1.5707, 0.0, yaw), 32, 32, flags=vx.FLAG_GLASS_SINGLE)
+    fo = vx.make_frame((x, 12.2, 5.4), (1.5707, 0.0, yaw), 32, 32)
     a, _ = Ob.render(fr.params, 32, 32)
     b, _ = Ob.render(fo.params, 32, 32)
     n = Ob.glass_layers(fr.params, 32, 32)
@@ -186,8 +186,8 @@ def test_glass_order_changes_only_stacked_pixels(O, noise):
     Ob = O.Oracle(f, noise, exit=True, quad=O.face_quads(f))
     tot = 0
     for rot in ((1.1, 0.0, 0.6), (1.2, 0.0, 2.6), (1.3, 0.0, -2.2)):
-        fr = vx.make_frame((48.0, 32.0, 20.0), rot, 128, 96, flags=vx.FLAG_FULL_QUALITY)
-        fo = vx.make_frame((48.0, 32.0, 20.0), rot, 128, 96, flags=vx.FLAG_FULL_QUALITY | 0x1000)
+        fr = vx.make_frame((48.0, 32.0, 20.0), rot, 128, 96, flags=vx.FLAG_FULL_QUALITY | vx.FLAG_GLASS_SINGLE)
+        fo = vx.make_frame((48.0, 32.0, 20.0), rot, 128, 96, flags=vx.FLAG_FULL_QUALITY)
         a, sa = Ob.render(fr.params, 128, 96)
         b, sb = Ob.render(fo.params, 128, 96)
         n = Ob.glass_layers(fr.params, 128, 96)
@@ -196,3 +196,34 @@ def test_glass_order_changes_only_stacked_pixels(O, noise):
         assert sa.glass_px == sb.glass_px
         tot += int(diff.sum())
     assert tot > 20
+
+
+def _many_panes(n_panes):
+    """n_panes glass panes, 2 cells apart, between a wall at x = 2 and a camera
+    at x ~ 45 looking toward -x: the far panes' quads are drawn first (lower
+    chunk, lower slice), so every pane blends (render.js:82-91)."""
+    X, Y, Z = 64, 24, 12
+    g = np.zeros((Z, Y, X), np.uint8)
+    g[0] = 2
+    g[1:10, 2:22, 2] = 9
+    for k in range(n_panes):
+        g[1:10, 2:22, 38 - 3 * k] = 21     # nearest at x = 38, then 35, 32, ...
+    return g
+
+
+def test_glass_order_blends_more_than_eight_panes(O, noise):
+    """Every pane a ray crosses takes part (no layer cap): with 10
+    panes the two farthest still change the pixels that see them."""
+    import voxmap_amd as vx
+    fr = vx.make_frame((45.0 - 5.4, 12.2, 5.4), (1.5707, 0.0, np.pi / 2), 32, 32)
+    imgs, layers = [], None
+    for n in (10, 8):
+        f = O.field_build(_many_panes(n))
+        Ob = O.Oracle(f, noise, quad=O.face_quads(f))
+        img, st = Ob.render(fr.params, 32, 32)
+        imgs.append(img)
+        if n == 10:
+            layers = Ob.glass_layers(fr.params, 32, 32)
+    assert (layers >= 9).sum() > 100, np.bincount(layers.ravel())
+    diff = np.any(imgs[0].view(np.uint32) != imgs[1].view(np.uint32), axis=2)
+    assert diff[layers >= 9].mean() > 0.9

@@ -110,16 +110,35 @@ def test_c3_unit_split_matches_oracle(noise, flags):
     _counters_equal(st, ost)
 
 
+@pytest.mark.parametrize("cam,flags", [("K0", 48), ("K1", 48), ("K2", 48), ("K1", 0)])
+def test_s_glass_c3_default_draw_order(noise, cam, flags):
+    """S-glass (panes that stack along view rays), C3, default flags: glass in
+    draw order (render.js:82-91) -- the stacked pixels' chain in the main
+    kernels -- every pixel and counter against the oracle."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_glass"))
+    fr = presets.camera_frame(cam, 3840, 2160, flags=flags)
+    with _scene(vx, field, noise, (1024, 256, 32)) as sc:
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 3840, 2160, threads=16)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+    assert st.glass_px > 100000
+
+
 @pytest.mark.parametrize("cam", ["K1", "K2"])
 def test_s_glass_c3_single_layer(noise, cam):
-    """S-glass (panes that stack along view rays), C3 full quality, the
-    single layer: every pixel and counter against the oracle."""
+    """S-glass, C3 full quality, the single layer (VX_FLAG_GLASS_SINGLE, the
+    ABI <= 8 default, kept as a diagnostic): every pixel and counter against
+    the oracle."""
     import oracle
     import voxmap_amd as vx
     from voxmap_amd import presets
     grid = presets.scene_grid("s_glass")
     field = vx.field_build(grid)
-    fr = presets.camera_frame(cam, 3840, 2160, flags=vx.FLAG_FULL_QUALITY)
+    fr = presets.camera_frame(cam, 3840, 2160, flags=vx.FLAG_FULL_QUALITY | vx.FLAG_GLASS_SINGLE)
     with _scene(vx, field, noise, (1024, 256, 32)) as sc:
         img, st = sc.render(fr, stats=True)
     ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 3840, 2160, threads=16)
@@ -158,13 +177,16 @@ GLASS_CASES = [
 
 
 @pytest.mark.parametrize("seed,dims,sbj,rot", GLASS_CASES)
-@pytest.mark.parametrize("flags,samples", [(0x1000, 0), (48 | 0x1000, 0), (0x2000 | 0x1000 | 32, 0),
-                                           (48 | 0x1000, 16), (48 | 0x1000 | 0x80, 16)],
-                         ids=["order_v1", "order_full", "order_reflect_all", "order_soft16", "order_soft16_pool"])
+@pytest.mark.parametrize("flags,samples", [(0, 0), (48, 0), (48, 16), (48 | 0x80, 16), (48 | 0x100, 16),
+                                           (0x1000, 0), (48 | 0x1000, 0), (0x2000 | 0x1000 | 32, 0), (0x2000 | 48, 0),
+                                           (48 | 0x1000, 16), (48 | 0x8000, 0)],
+                         ids=["v1", "full", "soft16", "soft16_pool", "soft16_brick", "general_v1", "general_full",
+                              "general_reflect_all", "reflect_all", "general_soft16", "single_full"])
 def test_glass_order_small(noise, seed, dims, sbj, rot, flags, samples):
-    """Glass in draw order (VX_FLAG_GLASS_ORDER, render.js:82-91) against the
-    oracle's restatement, every pixel and counter; the frame differs from the
-    single layer on the pixels whose ray crosses two or more panes."""
+    """Glass in draw order (render.js:82-91), the default -- in the main kernels
+    (EXT 0-4) and in the general ones (VX_FLAG_GLASS_ORDER, REFLECT_ALL: EXT 5/6)
+    -- and the single-layer diagnostic, against the oracle's restatement, every
+    pixel and counter."""
     import oracle
     import voxmap_amd as vx
     from voxmap_amd import scenes
@@ -225,3 +247,21 @@ def test_reflect_all_c3(noise):
     _compare(img, ref)
     _counters_equal(st, ost)
     assert st.reflect_rays > 6_000_000
+
+
+def test_glass_more_than_eight_panes(noise):
+    """Ten stacked panes, all drawn far to near (every one blends): the default
+    kernels and the general ones against the oracle (no layer cap)."""
+    import oracle
+    import voxmap_amd as vx
+    from test_quad_gbuf import _many_panes
+    field = vx.field_build(_many_panes(10))
+    O = oracle.Oracle(field, noise, exit=True)
+    for flags in (48, 48 | 0x1000):
+        fr = vx.make_frame((45.0 - 5.4, 12.2, 5.4), (1.5707, 0.0, np.pi / 2), 64, 64, flags=flags)
+        with _scene(vx, field, noise, (64, 24, 12)) as sc:
+            img, st = sc.render(fr, stats=True)
+        ref, ost = O.render(fr.params, 64, 64)
+        _compare(img, ref)
+        _counters_equal(st, ost)
+        assert (O.glass_layers(fr.params, 64, 64) >= 9).sum() > 400

@@ -32,12 +32,12 @@ FLAG_SOFT_BRICK = 0x100                         # + LDS 8^3 brick staging (same 
 FLAG_NO_EXIT = 0x200                            # diagnostics: march without the sun exit tables (same frames)
 FLAG_NO_CONE = 0x400                            # diagnostics: orthant exit tables only (same frames)
 FLAG_UNIT_GBUF = 0x800                          # diagnostics: the unit-cell G-buffer split (ABI <= 7)
-FLAG_GLASS_ORDER = 0x1000                       # every pane in draw order (render.js:82-91), not one layer
+FLAG_GLASS_ORDER = 0x1000                       # diagnostics: the whole frame through the general draw-order kernel
+FLAG_GLASS_SINGLE = 0x8000                      # diagnostics: nearest pane only (ABI <= 8); default = draw order
 FLAG_REFLECT_ALL = 0x2000                       # ext: every first surface mirrors the scene
 FLAG_ROWS_BOTTOM_UP = 0x4000                    # diagnostics: blocks dispatched bottom row first (same frames)
-MAX_GLASS_LAYERS = 8
 MAX_SHADOW_SAMPLES = 16
-ABI_VERSION = 8
+ABI_VERSION = 9
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128
 
@@ -124,6 +124,7 @@ SIGNATURES = [
     ("vx_mgpu_rank", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("vx_mgpu_destroy", None, [C.c_void_p]),
     ("vx_mgpu_bands", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int]),
+    ("vx_mgpu_band_rows", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("vx_mgpu_transfers", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]),
     ("vx_frame_from_orbit", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
                                       C.POINTER(FrameParams)]),

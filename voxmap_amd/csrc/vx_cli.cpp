@@ -193,8 +193,9 @@ int main(int argc, char **argv) {
         close(uid_pipe[0]); close(uid_pipe[1]);
         check(vx_mgpu_create(scene, uid, nranks, rank, &mg), "vx_mgpu_create");
     }
+    const int band_rows = vx_mgpu_band_rows(h, nranks > 0 ? nranks : 1, 64);   // the balanced deal
     auto draw = [&](vx_stats *s) {
-        if (mg) check(vx_mgpu_render(mg, &p, w, h, 64, VX_PIXEL_RGBA8, d_out, stream, s), "vx_mgpu_render");
+        if (mg) check(vx_mgpu_render(mg, &p, w, h, band_rows, VX_PIXEL_RGBA8, d_out, stream, s), "vx_mgpu_render");
         else check(vx_render(scene, &p, w, h, VX_PIXEL_RGBA8, d_out, 1, stream, s), "vx_render");
     };
     vx_stats st = {};

@@ -677,7 +677,9 @@ __device__ __forceinline__ void qcopy_offsets(uint32_t w, int ax, float &o0, flo
 // colour 1..21, vx_scene_create) from a cell of another colour.  Air (map.bin
 // B = pal_size = 22, sdf.cpp:229-233) is never meshed (sdf.cpp:284), so a
 // glass -> air step is no surface: glass blends over the next entry behind
-// it (later glass entries are skipped: one blend layer).  Box-exit
+// it.  The walk records the nearest glass entry and the surface behind it;
+// a second glass entry before that surface sets `multi` (the panes' draw
+// order then decides the pixel: k_render's stacked pass, glass_scan).  Box-exit
 // stepping (oracle/vxo_render.c vxo_primary): in the ray octant's field copy
 // the extents E of a cell say the box [c, c + E*s] ahead of it is air, so one
 // step goes to the face where the ray leaves that box (E = 0: an exact DDA
@@ -694,7 +696,7 @@ __device__ __forceinline__ void qcopy_offsets(uint32_t w, int ax, float &o0, flo
 // [c, c + E*s] lies ahead of the ray: h and A bracket it on every axis.
 template <bool F32IDX>
 __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, float d1, float d2, Surf &g0, Surf &g1,
-                       Counters &cnt, float &t_hit) {
+                       Counters &cnt, float &t_hit, int &multi) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
     const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
@@ -781,7 +783,7 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     // entry is recorded, then 256 (matches nothing).  The sentinel's colour
     // byte 0xFF is no vis colour (those are 0..21), so leaving the grid is an
     // entry that stops the walk.
-    int gmark = kGlass, stop, col;
+    int gmark = kGlass, stop, col, mul = 0;
     float g0h = 0.0f, g1h = 0.0f, g2h = 0.0f, gt = 0.0f, te;
     float tb0, tb1, tb2;
     int gax = 0;
@@ -810,13 +812,17 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
         // a face of the mesh: entering a meshed cell (vis colour != 0) from a
         // cell of another colour; air is never meshed (sdf.cpp:229-233,284)
         const bool enter = col != prev && col != 0;
-        if (enter && col == gmark) {                   // first glass: blend over the next surface
-            gmark = 256;
-            g0h = h0; g1h = h1; g2h = h2; gt = te;
-            gax = e0 ? 0 : (e1 ? 1 : 2);
-            if (QSPEC) gqw = qw;
+        if (enter && col == kGlass) {                  // a glass entry (rare, divergent)
+            if (gmark == kGlass) {                     // the first: blend over the next surface
+                gmark = 256;
+                g0h = h0; g1h = h1; g2h = h2; gt = te;
+                gax = e0 ? 0 : (e1 ? 1 : 2);
+                if (QSPEC) gqw = qw;
+            } else {
+                mul = 1;                               // a second pane in front of the surface
+            }
         }
-        stop = (enter && col != kGlass) ? 1 : 0;       // later glass entries: single layer
+        stop = (enter && col != kGlass) ? 1 : 0;       // later glass entries are passed (the stacked pass blends them)
         asm volatile("" : "+v"(stop));                 // keep the lane flag in a VGPR
         prev = col;
         E0 = cvt_f32_ubyte1(t); E1 = cvt_f32_ubyte2(t); E2 = cvt_f32_ubyte3(t);
@@ -824,7 +830,8 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     } while (stop == 0 && ++it < cap);
     // opaque after the loop: otherwise the compiler keeps the loop's compare
     // masks (stop, tb == te) alive past it, at 3 SALU merges per mask per step
-    asm volatile("" : "+v"(col), "+v"(stop), "+v"(tb0), "+v"(tb1), "+v"(te));
+    asm volatile("" : "+v"(col), "+v"(stop), "+v"(tb0), "+v"(tb1), "+v"(te), "+v"(mul));
+    multi = mul;
     if (stop == 0) cnt.cap_hit++;
     const bool hit = stop != 0 && t < kSentinel;
     const int hax = tb0 == te ? 0 : (tb1 == te ? 1 : 2);    // exit axis of the last step (ties x < y < z)
@@ -915,15 +922,17 @@ __device__ __forceinline__ unsigned long long face_key(const KernelArgs &a, int 
 }
 
 // One pass over the view ray's glass faces (the walk of primary visibility,
-// scalar form like walk_reflect; oracle walk() with glass_layer 2): of the
-// nearest VX_MAX_GLASS_LAYERS front-facing glass entries before the first
-// opaque entry, the one drawn first after key `klast` (none: have_last false)
-// among those nearer than tmax.  Returns false if there is none; else its
-// G-buffer record (quad-relative unless a.quad_gbuf is 0), depth and key.
-// Its fetches repeat the primary walk's and are not counted again.
+// scalar form like walk_reflect; oracle walk() with glass_layer 3): of the
+// front-facing glass entries before the first opaque entry, the one drawn
+// first after key `klast` (none: have_last false) among those nearer than
+// tmax.  Returns false if there is none; else its G-buffer record
+// (quad-relative unless a.quad_gbuf is 0), depth and key, and whether it is
+// the ray's nearest pane.  No storage per pane, so a pixel blends every pane
+// its ray crosses, as the raster does.  Its fetches repeat the primary walk's
+// and are not counted again.
 __device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float d1, float d2, bool have_last,
                                            unsigned long long klast, float tmax, Surf &h, float &t_out,
-                                           unsigned long long &k_out) {
+                                           unsigned long long &k_out, bool &nearest) {
     const FrameConsts &F = a.fc;
     const float o0 = F.cam_fract[0], o1 = F.cam_fract[1], o2 = F.cam_fract[2];
     const int cc0 = F.cam_cell[0], cc1 = F.cam_cell[1], cc2 = F.cam_cell[2];
@@ -957,8 +966,8 @@ __device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float 
     const int st0 = d0 > 0.0f ? 1 : -1, st1 = d1 > 0.0f ? 1 : -1, st2 = d2 > 0.0f ? 1 : -1;
     uint32_t t = fetch(c0 + cc0, c1 + cc1, c2 + cc2);
     int prev = t & 0xff, e0 = (int)((t >> 8) & 0xff), e1 = (int)((t >> 16) & 0xff), e2 = (int)(t >> 24);
-    bool found = false;
-    int nglass = 0, bx = 0, by = 0, bz = 0, bax = 0, bst = 0;
+    bool found = false, bfirst = false, first = true;
+    int bx = 0, by = 0, bz = 0, bax = 0, bst = 0;
     unsigned bq = 0;
     float bt = 0.0f;
     unsigned long long bk = 0;
@@ -985,19 +994,18 @@ __device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float 
         e0 = (int)((t >> 8) & 0xff); e1 = (int)((t >> 16) & 0xff); e2 = (int)(t >> 24);
         if (col != prev && col != 0) {             // a front face
             if (col != kGlass) break;              // the opaque surface: no glass behind it is drawn
-            if (nglass < VX_MAX_GLASS_LAYERS) {
-                nglass++;
-                const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
-                const int nidx = 2 * ax + (stp > 0 ? 1 : 0);
-                unsigned q = a.qface[(size_t)nidx * a.XYZ + lin_index(a, x, y, z)];
-                q = q == 0xFFFFu ? 0u : q;
-                const unsigned long long k = face_key(a, x, y, z, nidx, q);
-                if ((!have_last || k > klast) && te < tmax && (!found || k < bk)) {
-                    found = true;
-                    bk = k; bt = te; bq = q; bax = ax; bst = stp;
-                    bx = c0; by = c1; bz = c2;
-                }
+            const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
+            const int nidx = 2 * ax + (stp > 0 ? 1 : 0);
+            unsigned q = a.qface[(size_t)nidx * a.XYZ + lin_index(a, x, y, z)];
+            q = q == 0xFFFFu ? 0u : q;
+            const unsigned long long k = face_key(a, x, y, z, nidx, q);
+            if ((!have_last || k > klast) && te < tmax && (!found || k < bk)) {
+                found = true;
+                bfirst = first;
+                bk = k; bt = te; bq = q; bax = ax; bst = stp;
+                bx = c0; by = c1; bz = c2;
             }
+            first = false;
         }
         prev = col;
     }
@@ -1020,6 +1028,7 @@ __device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float 
     h.f2 = bax == 2 ? 0.0f : (o2 + bt * d2) - (float)(bz - of2);
     t_out = bt;
     k_out = bk;
+    nearest = bfirst;
     return true;
 }
 
@@ -1434,6 +1443,47 @@ __device__ __forceinline__ void reflect_color(const KernelArgs &a, const Surf &g
     out[0] = rgba[0]; out[1] = rgba[1]; out[2] = rgba[2];
 }
 
+// Glass in draw order (render.js:82-91; DESIGN.md §5 "Glass"): the reference
+// draws the glass quads after every opaque one, in vertex.bin order, depth test
+// LESS with writes on, SRC_ALPHA blending -- a pane is blended iff it is
+// nearer than the last surface written when its quad is drawn.  The nearest
+// pane P1 of a ray is nearer than every other surface, so it always passes and
+// is always the last pane blended: the pixel is P1 over dst', where dst' is the
+// surface behind the panes with the panes drawn before P1 (key order, each
+// nearer than the last one written) blended over it.  glass_chain turns dst
+// (the surface behind, depth its depth) into dst'; k_render's one-blend path
+// then blends P1 (g[0]) over it.  It runs for pixels whose ray crosses two or
+// more panes in front of its surface (primary()'s multi): with one pane dst' =
+// dst.
+template <int XE>
+__device__ __forceinline__ void glass_chain(const KernelArgs &a, float d0, float d1, float d2, float dst[4], float depth,
+                                            Counters &cnt) {
+    const FrameConsts &F = a.fc;
+    unsigned long long klast = 0;
+    bool have_last = false, nearest = false;
+    Surf cur;
+    float tc;
+    unsigned long long kc;
+    while (glass_scan(a, d0, d1, d2, have_last, klast, depth, cur, tc, kc, nearest) && !nearest) {
+        depth = tc; klast = kc; have_last = true;
+        float src[4], rd[3];
+        shade_block<XE>(a, cur, src, cnt, false, 0.0f, 0.0f, 0.0f, rd);
+        if (XE && (F.flags & (VX_FLAG_REFLECT | VX_FLAG_REFLECT_ALL))) {   // ext REFLECT: panes mirror
+            float refl[3];
+            reflect_color<XE>(a, cur, rd, refl, cnt);
+            const int ax = cur.nidx >> 1;
+            const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
+            const float x = 1.0f - cs, x2 = x * x;
+            const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
+#pragma unroll
+            for (int i = 0; i < 3; i++) src[i] = src[i] + fr * refl[i];
+        }
+        const float al = src[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) dst[i] = src[i] * al + dst[i] * (1.0f - al);
+    }
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned v) {
     unsigned long long s = v;
 #pragma unroll
@@ -1644,12 +1694,17 @@ void k_render(KernelArgs a) {
         const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
         Surf g[2];
         float t_hit;
-        const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt, t_hit);
-        // glass in draw order and REFLECT_ALL: instantiations of their own (EXT 5, 6), so
-        // the walk over every pane of a pixel (glass_scan) and the mirror walk of every
-        // surface add no code or registers to the others (one shading loop there, the
-        // reference's single site here: measured 4 % on C3 full quality when shared)
-        const bool order = kGeneral && (F.flags & VX_FLAG_GLASS_ORDER);
+        int multi;
+        const int n = primary<F32IDX>(a, oct, d0, d1, d2, g[0], g[1], cnt, t_hit, multi);
+        // glass in draw order (render.js:82-91): the nearest pane is blended last,
+        // over what is behind it; a ray that crosses two or more panes in front
+        // of its surface first blends the panes drawn before the nearest one over
+        // that (glass_chain), with one pane there are none.  VX_FLAG_GLASS_SINGLE:
+        // the nearest pane only (diagnostic).  The general modes (VX_FLAG_GLASS_ORDER,
+        // REFLECT_ALL) are instantiations of their own (EXT 5, 6), so their mirror
+        // walk per surface adds no code or registers here.
+        const bool order = !(F.flags & VX_FLAG_GLASS_SINGLE);
+        const bool stacked = multi != 0 && order && !(F.flags & VX_FLAG_PRIMARY_ONLY) && inframe;
         int lit0 = -1;
         if (kPool && !inframe) cnt = Counters{};
         if (kPool && F.soft_sg >= 0 && a.sunp) {
@@ -1662,7 +1717,7 @@ void k_render(KernelArgs a) {
             // the others.  Same exact march_pad, lit counted per fragment in LDS.
             // (a glass pixel in draw order may shade other panes first: it marches in shade_block)
             const bool need = inframe && n != 0 && !(F.flags & (VX_FLAG_PRIMARY_ONLY | VX_FLAG_NO_SHADOW)) &&
-                              !(order && g[0].id == 2) && block_shade_factor<XE>(a, g[0]) > 0.0f;
+                              block_shade_factor<XE>(a, g[0]) > 0.0f;
             const unsigned long long mask = __ballot(need);
             if (mask) {
                 const int wb = threadIdx.x & ~63;                // this wave's 64 slots
@@ -1771,6 +1826,10 @@ if constexpr (!kGeneral) {
                 if (g[0].id == 2) {
                     if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
                     else shade_sky(a, d0, d1, d2, dst, cnt);
+                    // two or more panes (rare: a wave-uniform branch): the panes drawn
+                    // before the nearest one, in draw order, over what is behind
+                    if (__builtin_expect(__ballot(stacked) != 0, 0) && stacked)
+                        glass_chain<XE>(a, d0, d1, d2, dst, n == 2 ? t_hit : kInf, cnt);
                 }
                 float rd[3];
                 shade_block<XE>(a, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
@@ -1794,50 +1853,35 @@ if constexpr (!kGeneral) {
                 }
                 (void)t_hit;
 } else {
+                // the general modes (REFLECT_ALL, VX_FLAG_GLASS_ORDER): every first
+                // surface may mirror the scene; glass as in the one-blend path
                 float dst[4];
                 const bool glass = g[0].id == 2;
                 if (glass) {
                     if (n == 2) shade_block<XE>(a, g[1], dst, cnt);
                     else shade_sky(a, d0, d1, d2, dst, cnt);
+                    if (__builtin_expect(__ballot(stacked) != 0, 0) && stacked)
+                        glass_chain<XE>(a, d0, d1, d2, dst, n == 2 ? t_hit : kInf, cnt);
                 }
-                // The first surface; for glass, the panes blended over what is
-                // behind: the nearest one (single layer), or in draw order each
-                // pane nearer than the last one written (order: glass_scan finds
-                // the next, render.js:82-91).  One shade_block site for all of them.
-                Surf cur = g[0];
-                float depth = n == 2 ? t_hit : kInf;
-                unsigned long long klast = 0;
-                bool have_last = false;
-                for (;;) {
-                    if (order && glass) {
-                        float tc;
-                        unsigned long long kc;
-                        if (!glass_scan(a, d0, d1, d2, have_last, klast, depth, cur, tc, kc)) break;
-                        depth = tc; klast = kc; have_last = true;
-                    }
-                    float rd[3];
-                    shade_block<XE>(a, cur, rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, order && glass ? -1 : lit0);
-                    // ext REFLECT (glass panes) / REFLECT_ALL (every first surface and pane)
-                    if (XE && (F.flags & (glass ? (VX_FLAG_REFLECT | VX_FLAG_REFLECT_ALL) : VX_FLAG_REFLECT_ALL))) {
-                        // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
-                        float refl[3];
-                        reflect_color<XE>(a, cur, rd, refl, cnt);
-                        const int ax = cur.nidx >> 1;
-                        const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
-                        const float x = 1.0f - cs, x2 = x * x;
-                        const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
+                float rd[3];
+                shade_block<XE>(a, g[0], rgba, cnt, false, 0.0f, 0.0f, 0.0f, rd, lit0);
+                // ext REFLECT (glass panes) / REFLECT_ALL (every first surface and pane)
+                if (XE && (F.flags & (glass ? (VX_FLAG_REFLECT | VX_FLAG_REFLECT_ALL) : VX_FLAG_REFLECT_ALL))) {
+                    // Schlick Fresnel, F0 = 0.04, on the geometric normal (cos = |rayDir| on the face axis)
+                    float refl[3];
+                    reflect_color<XE>(a, g[0], rd, refl, cnt);
+                    const int ax = g[0].nidx >> 1;
+                    const float cs = gmin(fabsf(ax == 0 ? rd[0] : (ax == 1 ? rd[1] : rd[2])), 1.0f);
+                    const float x = 1.0f - cs, x2 = x * x;
+                    const float fr = 0.04f + 0.96f * ((x2 * x2) * x);
 #pragma unroll
-                        for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
-                    }
-                    if (!glass) break;
-                    const float al = rgba[3];
-#pragma unroll
-                    for (int i = 0; i < 3; i++) dst[i] = rgba[i] * al + dst[i] * (1.0f - al);
-                    if (!order) break;
+                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
                 }
                 if (glass) {
                     n_glass = 1;
-                    rgba[0] = dst[0]; rgba[1] = dst[1]; rgba[2] = dst[2];
+                    const float al = rgba[3];
+#pragma unroll
+                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
                 } else {
                     n_block = 1;
                 }

@@ -27,6 +27,24 @@ def bands(h: int, band_rows: int, world: int, rank: int) -> list:
     return list(range(rank, n_bands(h, band_rows), world))
 
 
+def band_rows_for(h: int, world: int, max_rows: int = 64) -> int:
+    """The deal's band height (vx_mgpu_band_rows): the multiple of 8 up to
+    max_rows whose round-robin deal gives the busiest rank the fewest rows,
+    ties to the tallest band (the fewest sends)."""
+    best, best_rows = 8, None
+    for r in range(8, max(8, max_rows - max_rows % 8) + 1, 8):
+        nb = n_bands(h, r)
+        busiest = max(sum(min(h, (b + 1) * r) - b * r for b in range(k, nb, world)) for k in range(min(world, nb)))
+        if best_rows is None or busiest <= best_rows:
+            best, best_rows = r, busiest
+    return best
+
+
+def rows_per_rank(h: int, band_rows: int, world: int) -> list:
+    return [sum(min(h, (b + 1) * band_rows) - b * band_rows for b in bands(h, band_rows, world, k))
+            for k in range(world)]
+
+
 def band_rows_of(b: int, h: int, band_rows: int) -> slice:
     return slice(b * band_rows, min(h, (b + 1) * band_rows))
 

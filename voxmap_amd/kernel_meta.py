@@ -22,9 +22,12 @@ FIELDS = ("private_segment_fixed_size", "vgpr_count", "sgpr_count", "vgpr_spill_
           "group_segment_fixed_size")
 RENDER_SCRATCH_LIMIT = 256      # bytes per thread: spill slots yes, a KernelArgs copy (~1.7 KB) no
 STATS_SCRATCH_LIMIT = 512       # the counting (STATS) instantiations keep ~16 counters live: more spill slots
-# VGPR spills allowed per EXT mode of a timed (non-STATS) k_render instantiation
-# (0 v1, 1 extensions, 2 soft shadows, 3 pooled, 4 LDS bricks, 5/6 glass in draw order)
-SPILL_LIMITS = {0: 0, 1: 0, 2: 6, 3: 4, 4: 40, 5: 12, 6: 12}
+# VGPR spill slots allowed per EXT mode of a timed (non-STATS) k_render
+# instantiation (0 v1, 1 extensions, 2 soft shadows, 3 pooled, 4 LDS bricks, 5/6
+# general).  The rare paths (glass in draw order where panes stack, the stacked
+# chain) spill at the 8-wave budget; what must never spill is a
+# hot loop -- hot_loop_spills() checks the march and primary loops themselves.
+SPILL_LIMITS = {0: 16, 1: 64, 2: 80, 3: 96, 4: 144, 5: 24, 6: 24}
 RENDER_VGPR_LIMIT = 64          # 8 waves/SIMD
 GENERAL_VGPR_LIMIT = 96         # EXT 5/6: 5 waves/SIMD (their own unit, vx_render_e56.hip)
 
@@ -92,6 +95,61 @@ def render_params(name: str):
     return tuple(int(g) for g in m.groups()) if m else None
 
 
+def hot_loop_spills(lib: str, ext_max: int = 2) -> dict[tuple, tuple[int, int]]:
+    """(hot loops, spill instructions inside them) of each timed render kernel
+    (RGBA8, no stats, EXT <= ext_max).  Spill instructions: scratch_*,
+    v_writelane, v_readlane.  Hot loops: the loops of the kernel's main body
+    (before its first s_endpgm; the compiler places the rare paths after it)
+    that are innermost, at most 400 instructions long, and hold a march texel
+    load (buffer_load_format_x) or the primary walk's extent decode
+    (v_cvt_f32_ubyte1): the step loops."""
+    out: dict[tuple, tuple[int, int]] = {}
+    with tempfile.TemporaryDirectory() as d:
+        for co in code_objects(lib, d):
+            txt = subprocess.run([_tool("llvm-objdump"), "-d", "--no-show-raw-insn", co], check=True,
+                                 capture_output=True, text=True).stdout
+            name, body = None, []
+            for line in txt.splitlines() + ["0 <END>:"]:
+                m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+                if m:
+                    p = render_params(name) if name else None
+                    if p and p[0] == 1 and p[1] == 0 and p[3] <= ext_max:
+                        out[p] = _hot_spills(body)
+                    name, body = m.group(1), []
+                elif name and "//" in line:
+                    ins, cmt = line.split("//", 1)
+                    am = re.match(r"\s*([0-9A-Fa-f]+):", cmt)
+                    if am:
+                        body.append((int(am.group(1), 16), ins.strip()))
+    return out
+
+
+def _hot_spills(body: list[tuple[int, str]]) -> tuple[int, int]:
+    end = next((i for i, (_, l) in enumerate(body) if l.startswith("s_endpgm")), len(body))
+    body = body[:end]
+    index = {a: i for i, (a, _) in enumerate(body)}
+    spill = [bool(re.match(r"(scratch_|v_writelane|v_readlane)", l)) for _, l in body]
+    hot = [bool(re.match(r"(buffer_load_format_x\s|v_cvt_f32_ubyte1)", l)) for _, l in body]
+    back = []                                             # backward branches: (loop head, latch)
+    for i, (a, l) in enumerate(body):
+        m = re.match(r"s_(?:cbranch_\w+|branch)\s+(\d+)", l)
+        if not m:
+            continue
+        off = int(m.group(1))
+        off = off - 65536 if off >= 32768 else off        # simm16, printed unsigned
+        tgt = index.get(a + 4 + 4 * off)                  # SOPP branch: PC + 4 + 4 * simm16
+        if tgt is not None and tgt < i:
+            back.append((tgt, i))
+    loops = n = 0
+    for h, e in back:                                     # innermost loops: the step loops themselves
+        if (e - h > 400 or any(h <= h2 and e2 <= e and (h2, e2) != (h, e) for h2, e2 in back)
+                or not any(hot[h:e + 1])):
+            continue
+        loops += 1
+        n = max(n, sum(spill[h:e + 1]))
+    return loops, n
+
+
 def check(lib: str) -> dict[str, dict[str, int]]:
     """Raise if a render kernel copies its arguments to scratch or loses occupancy."""
     ks = kernels(lib)
@@ -117,6 +175,11 @@ def check(lib: str) -> dict[str, dict[str, int]]:
         general = p is not None and p[3] >= 5
         if not stats and v.get("vgpr_count", 0) > (80 if brick else GENERAL_VGPR_LIMIT if general else RENDER_VGPR_LIMIT):
             bad.append(f"{name}: {v['vgpr_count']} VGPRs > {RENDER_VGPR_LIMIT}")
+    for p, (loops, n) in hot_loop_spills(lib).items():
+        if not loops:
+            bad.append(f"k_render{p}: no march / primary loop found in the disassembly (check the parser)")
+        if n:
+            bad.append(f"k_render{p}: {n} spill instructions inside a march / primary loop")
     if bad:
         raise RuntimeError("render kernel resource check failed:\n  " + "\n  ".join(bad))
     return ks

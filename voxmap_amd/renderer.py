@@ -272,6 +272,13 @@ def mgpu_bands(h: int, band_rows: int, nranks: int, rank: int) -> list:
     return list(ids[:n])
 
 
+def mgpu_band_rows(h: int, nranks: int, max_rows: int = 64) -> int:
+    """The deal's band height for an h-row frame over nranks ranks (vx_mgpu_band_rows)."""
+    r = lib().vx_mgpu_band_rows(int(h), int(nranks), int(max_rows))
+    check(r if r < 0 else 0)
+    return r
+
+
 def mgpu_transfers(w: int, h: int, band_rows: int, nranks: int, rank: int, pixel_format: int = 1) -> list:
     """The gather's transfer list as ``rank`` issues it (vx_mgpu_transfers, a pure
     host function): [(band, src, dst, rows, byte offset, bytes), ...] in band order."""
