@@ -186,3 +186,112 @@ def test_c3_full_size_no_exit_equals_exit_tables(noise, flags):
     assert sb.shadow_fetches > 3 * sa.shadow_fetches
     _, ost = oracle.Oracle(field, noise).render(fn.params, 3840, 2160, row0=0, row_step=1, threads=16)
     assert sb.shadow_fetches == ost.shadow_fetches and sb.primary_fetches == ost.primary_fetches
+
+
+# ---- full-size evidence that the exit tables change no pixel ----
+def _literal_subset(sc, fr, W, H, O, every=16):
+    """The frame marched WITHOUT exit tables (VX_FLAG_NO_EXIT, every step of
+    render.frag:92-136) on a band subset (8-row bands 0, every, 2*every, ...:
+    rows j + 8*every*k, j < 8) against the oracle's literal march
+    (Oracle(exit=False)) on the same rows: every fp32 word and every work
+    counter.  Returns the device's subset rows."""
+    import torch
+
+    import voxmap_amd as vx
+    assert fr.params.flags & vx.FLAG_NO_EXIT
+    ids = list(range(0, -(-H // 8), every))
+    out = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    st = sc.render_bands(fr, 8, ids, out.data_ptr(), inplace=True, pixel_format=vx.PIXEL_RGBA32F, stats=True)
+    torch.cuda.synchronize()
+    img = out.cpu().numpy()
+    del out
+    ref = np.full((H, W, 4), np.nan, np.float32)
+    acc = {}
+    for j in range(8):
+        _, ost = O.render(fr.params, W, H, row0=j, row_step=8 * every, threads=16, out=ref)
+        for k, v in ost.as_dict().items():
+            acc[k] = acc.get(k, 0) + v
+    rows = [r for b in ids for r in range(8 * b, min(H, 8 * b + 8))]
+    a, b = img[rows], ref[rows]
+    assert not np.isnan(a).any() and not np.isnan(b).any()
+    assert acc["pixels"] == len(rows) * W and acc["shadow_fetches"] > 0
+    bad = int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32)))
+    assert bad == 0, f"{bad} words differ from the literal march"
+    g = st.as_dict()
+    for k, v in acc.items():
+        assert g[k] == v, (k, g[k], v)
+    return rows, a
+
+
+def _frames_equal_and_literal(sc, fr_default, fr_literal, W, H, O):
+    """The default frame (exit tables) equals the literal frame on every pixel
+    (both on the device, RGBA32F), and the literal frame's band subset equals
+    the oracle's literal march, counters included."""
+    import voxmap_amd as vx
+    a, sa = sc.render(fr_default, stats=True)
+    b, sb = sc.render(fr_literal, stats=True)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sb.shadow_fetches > sa.shadow_fetches
+    rows, sub = _literal_subset(sc, fr_literal, W, H, O)
+    assert np.array_equal(sub.view(np.uint32), b[rows].view(np.uint32))
+    return sa, sb
+
+
+def test_c5_full_size_literal_march(noise):
+    """C5 (3^3-upscaled 3072x768x96 field, 3840x2160, 16-sample soft shadows,
+    full quality): the default frame -- cone exit table, the first-step face-bit
+    test that settles all 16 samples at once -- equals the frame marched
+    without tables on every pixel, and a band subset of that frame equals the
+    oracle's literal march, every word and counter."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    grid = presets.scene_grid("s_up3")
+    Z, Y, X = grid.shape
+    c = presets.CONFIGS["C5"]
+    kw = dict(scale=3.0, shadow_samples=16, sun_radius=0.03)
+    fd = presets.camera_frame("K1", c["w"], c["h"], flags=vx.FLAG_FULL_QUALITY, **kw)
+    fl = presets.camera_frame("K1", c["w"], c["h"], flags=vx.FLAG_FULL_QUALITY | vx.FLAG_NO_EXIT, **kw)
+    with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
+        del grid
+        field = sc.read_field(0)
+        oct_e = [np.ascontiguousarray(sc.read_boxes(o)[..., 1:]) for o in range(8)]
+        O = oracle.Oracle(field, noise, oct_e=oct_e, exit=False)
+        sa, sb = _frames_equal_and_literal(sc, fd, fl, c["w"], c["h"], O)
+    assert sa.shadow_rays_resolved > 0 and sb.shadow_rays_resolved == 0
+
+
+def test_c3_reflect_all_full_size_literal_march(noise):
+    """C3 K1 full quality + REFLECT_ALL (the general kernel, every first surface
+    mirrored): exit tables vs none, and the literal march against the oracle."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_proc"))
+    f = vx.FLAG_FULL_QUALITY | vx.FLAG_REFLECT_ALL
+    fd = presets.camera_frame("K1", 3840, 2160, flags=f)
+    fl = presets.camera_frame("K1", 3840, 2160, flags=f | vx.FLAG_NO_EXIT)
+    with vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=(1024, 256, 32), device=0) as sc:
+        sa, _ = _frames_equal_and_literal(sc, fd, fl, 3840, 2160, oracle.Oracle(field, noise, exit=False))
+    assert sa.reflect_rays > 6_000_000
+
+
+@pytest.mark.parametrize("order", [0, 0x1000], ids=["default", "general"])
+def test_s_glass_c3_full_size_literal_march(noise, order):
+    """S-glass C3 K1 full quality, glass in draw order -- the default (stacked
+    chain in the main kernel) and VX_FLAG_GLASS_ORDER (the general kernel): the
+    march runs once per blended pane; exit tables vs none, and the literal
+    march against the oracle."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import presets
+    field = vx.field_build(presets.scene_grid("s_glass"))
+    f = vx.FLAG_FULL_QUALITY | order
+    fd = presets.camera_frame("K1", 3840, 2160, flags=f)
+    fl = presets.camera_frame("K1", 3840, 2160, flags=f | vx.FLAG_NO_EXIT)
+    with vx.Scene(map_bytes=field.tobytes(), map_format=vx.FORMAT_BIN, noise_bytes=noise.tobytes(),
+                  noise_format=vx.FORMAT_BIN, dims=(1024, 256, 32), device=0) as sc:
+        sa, _ = _frames_equal_and_literal(sc, fd, fl, 3840, 2160, oracle.Oracle(field, noise, exit=False))
+    assert sa.glass_px > 100000
