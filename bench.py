@@ -587,7 +587,12 @@ def main(argv=None):
                 "alg_bytes": int(sr["alg_bytes"]), "roofline_frac": round(roofline_of(sr["alg_bytes"], c["ev_ms"])[1], 4),
                 "timing": c["blocks"]}
 
-    rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]   # rays actually marched per frame
+    # rays per frame: primary + shadow + reflection rays resolved.  With soft
+    # shadows some shadow rays are settled by one exit-table test of the
+    # fragment's first step (shadow_rays_resolved) instead of a
+    # march; rays_marched_per_frame / mrays_per_s_marched count only the marched ones
+    rays = stats["pixels"] + stats["shadow_rays"] + stats["reflect_rays"]
+    marched = rays - stats.get("shadow_rays_resolved", 0)
     value = rays * args.steps / wall / 1e6                                   # whole-job Mrays/s
     result = None
     if rank == 0:
@@ -630,7 +635,7 @@ def main(argv=None):
                     f"v1 shading flags={flags}") +
                     (f" + {samples}-sample soft shadows (sun radius {args.sun_radius})" if samples > 1 else "") +
                     f", field {X}x{Y}x{Z}, camera {cam}, sun hour 1.0, RGBA8 framebuffer in HBM",
-                "value_is": (f"rays marched per second over {K} frames in flight ({K} streams, {K} framebuffers), "
+                "value_is": (f"rays per second (primary + shadow + reflection; rays_marched_per_frame excludes soft-shadow rays settled by the first-step table test) over {K} frames in flight ({K} streams, {K} framebuffers), "
                              "inputs and framebuffers HBM-resident; the roofline uses the one-stream launch time"
                              if world == 1 else
                              f"rays marched per second by all {world} ranks, the RCCL gather to rank 0 inside "
@@ -644,7 +649,8 @@ def main(argv=None):
                 "fps_with_d2h": d2h,
                 "inflight": {"frames": K, "streams": K, "framebuffers": K,
                              "single_stream_ms_per_frame": round(ev_ms, 4) if ev_ms is not None else None},
-                "rays_per_frame": int(rays), "primary_rays": int(stats["pixels"]),
+                "rays_per_frame": int(rays), "rays_marched_per_frame": int(marched),
+                "mrays_per_s_marched": round(marched * args.steps / wall / 1e6, 3), "primary_rays": int(stats["pixels"]),
                 "shadow_rays": int(stats["shadow_rays"]), "reflect_rays": int(stats["reflect_rays"]),
                 "lane_util": lane_utils(stats) if world == 1 else None,
                 "exit_tables": exit_info,

@@ -123,9 +123,10 @@ def test_two_threads_cycle_three_suns(scene):
     """two host threads render one scene on their own streams while
     cycling through three suns with different cone windows (two cache slots, so
     slots are recycled while the other thread's frames may still read them).
-    A slot is pinned from its lookup until the render that reads it is enqueued
-    and recorded as its reader; recycling waits for those readers.  Every frame
-    equals the same frame rendered alone."""
+    A slot is pinned from its lookup until the render that reads it is enqueued,
+    and keeps the streams such renders went to; a recycle makes the building
+    stream wait for the work enqueued so far on each of them (vx_api.cpp
+    cone_copy).  Every frame equals the same frame rendered alone."""
     import threading
 
     import torch
@@ -152,6 +153,51 @@ def test_two_threads_cycle_three_suns(scene):
                     sc.render_device(frames[k], bufs[j].data_ptr(), pixel_format=vx.PIXEL_RGBA8,
                                      stream=st.cuda_stream)
                 st.synchronize()
+                for j, k in enumerate(order):
+                    if not np.array_equal(bufs[j].cpu().numpy(), refs[k]):
+                        errors.append((tid, rep, k))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append((tid, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_two_threads_per_thread_stream_cycle_three_suns(scene):
+    """hipStreamPerThread is one handle that names a different
+    stream on each host thread.  Two threads pass it while cycling three cone
+    windows through the two slots: a slot one of them read is recycled only
+    after a device-wide wait (no handle names the reader's stream), and a cache
+    hit always waits for the build.  Every frame equals the frame rendered alone."""
+    import threading
+
+    import torch
+
+    import voxmap_amd as vx
+    sc, _ = scene
+    W, H = 192, 120
+    per_thread = 2                                   # hipStreamPerThread (hip_runtime_api.h)
+    suns = [(31, 40), (44, 130), (57, 220)]
+    frames = {k: vx.make_frame((64.0, 32.0, 34.0), (1.0, 0.0, -0.4), W, H, sun=_sun(*k),
+                               flags=vx.FLAG_FULL_QUALITY) for k in suns}
+    refs = {}
+    for k, fr in frames.items():
+        r = sc.render(fr, pixel_format=vx.PIXEL_RGBA8)
+        refs[k] = np.ascontiguousarray(r[0] if isinstance(r, tuple) else r).view(np.uint8).ravel()
+    errors = []
+
+    def worker(tid):
+        try:
+            bufs = [torch.empty(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(3)]
+            for rep in range(10):
+                order = suns if tid == 0 else suns[::-1]
+                for j, k in enumerate(order):
+                    sc.render_device(frames[k], bufs[j].data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=per_thread)
+                torch.cuda.synchronize()
                 for j, k in enumerate(order):
                     if not np.array_equal(bufs[j].cpu().numpy(), refs[k]):
                         errors.append((tid, rep, k))

@@ -265,3 +265,33 @@ def test_glass_more_than_eight_panes(noise):
         _compare(img, ref)
         _counters_equal(st, ost)
         assert (O.glass_layers(fr.params, 64, 64) >= 9).sum() > 400
+
+
+def test_scene_without_face_table(noise, monkeypatch):
+    """a field whose face table does not fit still loads (the
+    allocation forced to fail); its 3D frames then need the unit-cell split
+    and the single glass layer -- the only ones that read no mesh -- and it
+    refuses the others with VX_EINVAL instead of rendering something else."""
+    import oracle
+    import voxmap_amd as vx
+    from voxmap_amd import scenes
+    dims = (96, 64, 16)
+    field = vx.field_build(scenes.s_glass(2, dims=dims, n_houses=12, n_facades=4))
+    monkeypatch.setenv("VOXMAP_TEST_NO_FACE_TABLE", "1")
+    sc = _scene(vx, field, noise, dims)
+    monkeypatch.delenv("VOXMAP_TEST_NO_FACE_TABLE")
+    with sc:
+        for flags in (48, 48 | vx.FLAG_UNIT_GBUF, 48 | vx.FLAG_GLASS_SINGLE,
+                      48 | vx.FLAG_UNIT_GBUF | vx.FLAG_GLASS_SINGLE | vx.FLAG_GLASS_ORDER):
+            with pytest.raises(vx.VoxmapError) as e:
+                sc.render(vx.make_frame((48.0, 32.0, 20.0), (1.1, 0.0, 0.6), 64, 48, flags=flags))
+            assert e.value.code == -1 and "face table" in str(e.value)
+        with pytest.raises(vx.VoxmapError):
+            sc.read_face_quads()
+        fr = vx.make_frame((48.0, 32.0, 20.0), (1.1, 0.0, 0.6), 200, 120,
+                           flags=48 | vx.FLAG_UNIT_GBUF | vx.FLAG_GLASS_SINGLE)
+        img, st = sc.render(fr, stats=True)
+    ref, ost = oracle.Oracle(field, noise, exit=True, quad=False).render(fr.params, 200, 120)
+    _compare(img, ref)
+    _counters_equal(st, ost)
+    assert st.glass_px > 500

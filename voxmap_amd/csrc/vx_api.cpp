@@ -36,13 +36,15 @@ struct vx_scene {
     struct Cone {
         int oct = -1, kx = -1, ky = -1;
         int8_t *d = nullptr;
-        hipEvent_t ready = nullptr;
+        hipEvent_t ready = nullptr;   // recorded on build_st after the build
+        hipStream_t build_st = nullptr;
         unsigned long long used = 0;
         bool ready_seen = false;      // the build's `ready` event observed complete
+        std::vector<hipStream_t> readers;   // streams a render reading this copy was enqueued on
+        bool any_reader_special = false;    // a reader passed hipStreamPerThread: no handle names its stream
     } cones[2];
     unsigned long long cone_tick = 0;
-    hipStream_t first_st = nullptr;   // the one stream cone copies were used on so far
-    bool any_st = false, multi_st = false;
+    hipEvent_t recycle_ev = nullptr;  // marks a reader stream's work at a recycle (cone_copy)
     std::mutex cone_mu;
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
@@ -224,11 +226,18 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
         // allocated after the arrays the kernels read every step: placed in front of them
         // it moved their device addresses, and the v1 frame measured 3.3 % slower with the
         // same kernel code (profiles/r04_ab_v1_bisect.txt, r04_ab_alloc_order.txt)
+        // Optional: a field whose table does not fit still loads; its
+        // frames then need the unit-cell split and the single glass layer
+        // (vx_render refuses others), which are the only ones that read no mesh.
+        // VOXMAP_TEST_NO_FACE_TABLE=1 makes the allocation fail (tests).
         if (!lrc) {
-            if ((e = hipMalloc(&s->d_qface, 3 * field_bytes)) == hipSuccess)
+            const char *no_tab = std::getenv("VOXMAP_TEST_NO_FACE_TABLE");
+            if ((no_tab && no_tab[0] == '1') || hipMalloc(&s->d_qface, 3 * field_bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                s->d_qface = nullptr;
+            } else {
                 lrc = launch_face_quads(lin, s->d_qface, X, Y, Z, in.chunk, s->stream);
-            else
-                lrc = (int)e;
+            }
         }
         // the fp32-index walk's companion copy: quad offsets loaded beside
         // every prim word; fields whose walk takes the integer index (or CHUNK > 32) read
@@ -238,7 +247,7 @@ int vx_scene_create(const vx_scene_desc *d, vx_scene **out) {
 #ifndef VX_QSPEC
 #define VX_QSPEC 1
 #endif
-        if (VX_QSPEC && !lrc && in.chunk <= 32 && f32_ok) {
+        if (VX_QSPEC && !lrc && s->d_qface && in.chunk <= 32 && f32_ok) {
             if (hipMalloc(&s->d_qcopy, 8 * L.texels * 4) != hipSuccess) {
                 (void)hipGetLastError();
                 s->d_qcopy = nullptr;
@@ -273,6 +282,7 @@ void vx_scene_destroy(vx_scene *s) {
         if (c.d) (void)hipFree(c.d);
         if (c.ready) (void)hipEventDestroy(c.ready);
     }
+    if (s->recycle_ev) (void)hipEventDestroy(s->recycle_ev);
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_rg2) (void)hipFree(s->d_rg2);
     if (s->d_noise4) (void)hipFree(s->d_noise4);
@@ -332,6 +342,7 @@ int vx_debug_block_times(vx_scene *s, unsigned long long *out, size_t cap, size_
 
 int vx_scene_read_face_quads(vx_scene *s, void *host_out, size_t cap) {
     if (!s || !host_out) return set_error(VX_EINVAL, "vx_scene_read_face_quads: null argument");
+    if (!s->d_qface) return set_error(VX_ENOMEM, "vx_scene_read_face_quads: the scene has no face table (it did not fit)");
     const size_t N = (size_t)s->X * s->Y * s->Z;
     if (cap < 12 * N) return set_error(VX_EINVAL, "vx_scene_read_face_quads: buffer too small");
     VX_HIP(hipSetDevice(s->device));
@@ -355,7 +366,15 @@ int vx_scene_read_boxes(vx_scene *s, int octant, void *host_out, size_t cap) {
 
 static int check_render(const vx_scene *s, const vx_frame_params *p, int w, int h, int fmt) {
     if (!s) return set_error(VX_EINVAL, "null scene/params");
-    return check_frame(p, w, h, fmt);
+    const int rc = check_frame(p, w, h, fmt);
+    if (rc) return rc;
+    // a scene without the greedy mesh per face (it did not fit) renders only
+    // what reads no mesh: the unit-cell split and the single glass layer
+    const unsigned need = VX_FLAG_UNIT_GBUF | VX_FLAG_GLASS_SINGLE;
+    if (!s->d_qface && p->quality != 0 && ((p->flags & need) != need || (p->flags & VX_FLAG_GLASS_ORDER)))
+        return set_error(VX_EINVAL, "this scene has no face table (it did not fit in device memory): its 3D frames "
+                                    "need VX_FLAG_UNIT_GBUF | VX_FLAG_GLASS_SINGLE and not VX_FLAG_GLASS_ORDER");
+    return VX_OK;
 }
 
 static void fill_stats(vx_stats *st, const unsigned long long *v, float ms, int out_bytes) {
@@ -395,20 +414,24 @@ struct TileSpec {
     int n = 0;
 };
 
-// The frame's cone copy {oct, kx, ky}: found in the scene's cache (the
-// stream waits for its build unless that is known complete or was enqueued on
-// the same single stream), or built on stream st into a free or the least
-// recently used slot -- after every render enqueued so far that reads that
-// slot has finished.  The caller holds s->cone_mu from here until its render
-// is enqueued, so every reader of a slot is enqueued before anyone can recycle
-// it; the recycle then waits for them by stream order (a scene used from one
-// stream, cone_stream) or one device-wide wait (several streams).  No reader
-// is tracked per render: an event recorded after every render is one more
-// stream packet between back-to-back frames, +3 % at C3
-// (profiles/r04_ab_event_c3.txt, r04_ab_multistream_events.txt), while a
-// recycle needs a third sun window in the scene's two slots.  t_build:
-// recorded on st just before the build's first packet (vx_prepare_sun's
-// timing), if built.
+// A stream handle that names one stream wherever it is used: not the
+// per-thread default stream, which is a different stream on every host thread.
+static bool plain_stream(hipStream_t st) { return st != hipStreamPerThread; }
+
+// The frame's cone copy {oct, kx, ky}: found in the scene's cache, or built on
+// stream st into a free or the least recently used slot.  The caller holds
+// s->cone_mu from here until its render is enqueued, so every render that
+// reads a slot is enqueued before anyone can recycle it, and the slot keeps
+// the streams those renders went to (`readers`).  A recycle then makes st wait
+// for the work enqueued so far on each reader stream -- one event recorded on
+// that stream now, one stream wait: stream-ordered, no host or device-wide
+// stall, nothing per render (an event after every render is one more stream
+// packet between back-to-back frames, +3 % at C3, profiles/r04_ab_event_c3.txt).
+// A reader that passed hipStreamPerThread names no stream another thread can
+// wait on: that slot's recycle waits for the device.  A cache hit
+// on a stream other than the build's waits for the build's event until the host
+// has seen it complete.  t_build: recorded on st just before the build's first
+// packet (vx_prepare_sun's timing), if built.
 static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built,
                      vx_scene::Cone **used, hipEvent_t t_build) {
     *built = false;
@@ -420,23 +443,35 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         for (auto &c : s->cones)
             if (!c.d || c.used < slot->used) slot = &c;
         if (slot->d) {
-            if (s->multi_st) VX_HIP(hipDeviceSynchronize());
+            if (slot->any_reader_special || !plain_stream(st)) {
+                VX_HIP(hipDeviceSynchronize());
+            } else {
+                if (!s->recycle_ev) VX_HIP(hipEventCreateWithFlags(&s->recycle_ev, hipEventDisableTiming));
+                for (hipStream_t r : slot->readers) {
+                    if (r == st) continue;                     // stream order
+                    VX_HIP(hipEventRecord(s->recycle_ev, r));
+                    VX_HIP(hipStreamWaitEvent(st, s->recycle_ev, 0));
+                }
+            }
         } else {
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
             VX_HIP(hipMalloc(&slot->d, np));
             if (!slot->ready) VX_HIP(hipEventCreateWithFlags(&slot->ready, hipEventDisableTiming));
         }
         slot->oct = -1;
+        slot->readers.clear();
+        slot->any_reader_special = false;
         if (t_build) VX_HIP(hipEventRecord(t_build, st));
         VX_HIP(hipMemsetAsync(slot->d, 0xFF, (size_t)s->SXp * s->SYp * s->SZp, st));
         const int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
         if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
         VX_HIP(hipEventRecord(slot->ready, st));
+        slot->build_st = st;
         slot->ready_seen = false;
         slot->oct = oct; slot->kx = kx; slot->ky = ky;
         *built = true;
-    } else if (s->multi_st && !slot->ready_seen) {       // one stream: built before it, in stream order
-        const hipError_t q = hipEventQuery(slot->ready);
+    } else if (!slot->ready_seen && (st != slot->build_st || !plain_stream(st))) {
+        const hipError_t q = hipEventQuery(slot->ready);   // another stream: wait for the build
         if (q == hipSuccess) slot->ready_seen = true;
         else if (q == hipErrorNotReady) VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));
         else VX_HIP(q);
@@ -447,17 +482,15 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
     return VX_OK;
 }
 
-// Before a lookup on stream st (cone_mu held): is the scene still used from
-// one stream only (cone_copy's waits)?
-static int cone_stream(vx_scene *s, hipStream_t st) {
-    if (s->multi_st) return VX_OK;
-    if (!s->any_st) {
-        s->any_st = true;
-        s->first_st = st;
-        return VX_OK;
+// A render on stream st reads `slot` (cone_mu held until it is enqueued).
+static void cone_reader(vx_scene::Cone *slot, hipStream_t st) {
+    if (!plain_stream(st)) {
+        slot->any_reader_special = true;
+        return;
     }
-    if (st != s->first_st) s->multi_st = true;
-    return VX_OK;
+    for (hipStream_t r : slot->readers)
+        if (r == st) return;
+    slot->readers.push_back(st);
 }
 
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
@@ -528,17 +561,16 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     a.max_shadow_steps = p->max_shadow_steps > 0 ? p->max_shadow_steps : 2 * s->Z;   // render.frag:12
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
     // the cone copy the frame reads stays pinned from its lookup until this
-    // render is enqueued and recorded as its reader (a second thread
-    // must not recycle it in between)
+    // render is enqueued (a second thread must not recycle it in
+    // between); its stream is kept as one of the copy's readers (cone_reader)
     std::unique_lock<std::mutex> cone_lock(s->cone_mu);
     vx_scene::Cone *cone = nullptr;
     {
-        int rc = cone_stream(s, st);
-        if (rc) return rc;
-        rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
+        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
         if (rc) return rc;
     }
-    if (!cone) cone_lock.unlock();
+    if (cone) cone_reader(cone, st);
+    else cone_lock.unlock();
     a.Xp = s->L.Xp;
     a.pad = s->L.pad;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
@@ -613,8 +645,6 @@ int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_
         // ev0 is recorded inside cone_copy right before the build's first packet:
         // build_ms is the copy's GPU time, not the host's allocation or waits
         std::lock_guard<std::mutex> lock(s->cone_mu);
-        rc = cone_stream(s, st);
-        if (rc) return rc;
         rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, s->ev0);
         if (rc) return rc;
         if (built) VX_HIP(hipEventRecord(s->ev1, st));
