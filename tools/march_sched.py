@@ -35,6 +35,49 @@ def lockstep(L, setup):
     return cost
 
 
+def sorted_pool(L, setup, group, pool_setup):
+    """Sample 0 of every lane in lockstep, then the remaining samples of the
+    marching fragments dealt in pooled passes of 64 // group fragments x group
+    lanes, fragments sorted by their sample-0 length (longest first): a pass
+    costs its longest march + pool_setup (the per-pass state reload)."""
+    cost = 0.0
+    col = L[:, 0]
+    if not (col >= 0).any():
+        return 0.0
+    cost += col.max() + setup
+    frags = [r for r in L if r[0] >= 0]
+    frags.sort(key=lambda r: -int(r[0]))
+    per = 64 // group
+    for i in range(0, len(frags), per):
+        rest = np.concatenate([r[1:][r[1:] >= 0] for r in frags[i:i + per]] + [np.zeros(0, np.int64)])
+        if rest.size:
+            cost += rest.max() + pool_setup
+    return cost
+
+
+def block_classes(L, setup, pool_setup):
+    """A 32x8 block (4 waves, L: (256, m)): sample 0 in lockstep per wave, then
+    every remaining march of the block dealt 64 at a time over the 4 waves,
+    the marches of fragments whose sample 0 ended unlit first (sorted by that
+    length), so a pass holds marches of one class: wave steps summed over the
+    block's waves."""
+    cost = 0.0
+    for w in range(4):
+        col = L[64 * w:64 * (w + 1), 0]
+        if (col >= 0).any():
+            cost += col.max() + setup
+    rest = []
+    for r in L:
+        if r[0] < 0:
+            continue
+        key = int(r[0])
+        rest += [(key, int(v)) for v in r[1:] if v >= 0]
+    rest.sort(key=lambda kv: -kv[0])
+    for i in range(0, len(rest), 64):
+        cost += max(v for _, v in rest[i:i + 64]) + pool_setup
+    return cost
+
+
 def refill(L, setup, threshold):
     queues = [list(r[r >= 0]) for r in L]
     cur = [q.pop(0) if q else -1 for q in queues]        # remaining steps of the running march
@@ -71,6 +114,7 @@ def main():
     fr = presets.camera_frame(cfg["camera"], W, H, flags=vx.FLAG_FULL_QUALITY, shadow_samples=args.samples,
                               sun_radius=0.03 if args.samples > 1 else 0.0)
     o = oracle.Oracle(field, noise, exit=True)
+    o.hold_exit_table(fr.params)
     L = oracle.lib()
     L.vxo_march_lengths.argtypes = [C.POINTER(oracle.OScene), C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_int, C.c_int, C.c_void_p, C.c_int]
@@ -100,6 +144,30 @@ def main():
         tot["ideal"] += buf[buf >= 0].sum() / 64.0
         for t in (4, 8, 16, 32):
             tot[f"refill_T{t}"] += refill(buf, args.setup, t)
+        if args.samples > 1:
+            tot["sorted_pool16"] = tot.get("sorted_pool16", 0.0) + sorted_pool(buf, args.setup, 16, 2 * args.setup)
+    if args.samples > 1:
+        # 32x8 blocks: lockstep vs the block-level two-class regroup
+        bl = {"lockstep": 0.0, "classes": 0.0, "ideal": 0.0}
+        nb = 0
+        for _ in range(args.tiles // 4):
+            px0 = int(rng.integers(0, W // 32)) * 32
+            py0 = int(rng.integers(0, H // 8)) * 8
+            buf = np.empty((8, 32, maxrec), np.int32)
+            L.vxo_march_lengths(C.byref(o.sc), C.addressof(fr.params), W, H, px0, py0, 32, 8, buf.ctypes.data,
+                                maxrec)
+            # lanes of wave w: columns 8w .. 8w+7 of the block's 8 rows
+            waves = np.concatenate([buf[:, 8 * w:8 * w + 8].reshape(64, maxrec) for w in range(4)])
+            m = waves >= 0
+            if not m.any():
+                continue
+            waves = np.where(m, waves & 0xFFFF, -1)
+            nb += 1
+            bl["lockstep"] += sum(lockstep(waves[64 * w:64 * (w + 1)], args.setup) for w in range(4))
+            bl["classes"] += block_classes(waves, args.setup, 2 * args.setup)
+            bl["ideal"] += waves[waves >= 0].sum() / 64.0
+        for k, v in bl.items():
+            print(f"  block {k:10s} {v / max(nb, 1):9.1f} wave steps per block ({v / bl['lockstep']:.3f} of lockstep)")
     print(f"{args.config} samples={args.samples} tiles with marches={n} setup={args.setup} steps")
     for k in ("fetch_lit", "fetch_unlit", "n_lit", "n_unlit"):
         print(f"  {k:12s} {tot.pop(k, 0)}")

@@ -1610,9 +1610,10 @@ __device__ __forceinline__ void shade_2d(const KernelArgs &a, float d0, float d1
 #define VX_OCC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_sgpr(80)))
 #endif
 // Workgroup = 256 threads = four 8x8-pixel waves side by side: a 32x8 pixel
-// block.  A 32-pixel block row is 128 B of RGBA8: the framebuffer store goes
-// through LDS so every wave writes two whole 128-B rows (full cache lines)
-// instead of eight 32-B pieces of its own 8x8 tile.
+// block.  Each wave stores its own 8x8 tile (32-B row pieces): staging the
+// block in LDS for whole 128-B rows needs a block barrier, and the waves of a
+// block finish at very different times (round 5: per-wave stores C3 full
+// quality -1.7 %, v1 -1.1 %, C5 -0.5..-1.2 %, profiles/r05_ab_wave_store_*.txt).
 constexpr int kBX = 32;                    // block width in pixels
 constexpr int kBY = kWG / kBX;             // block height
 constexpr int kBXS = 5;                    // log2(kBX)
@@ -1623,8 +1624,14 @@ static_assert(kBX == 1 << kBXS && kBY == 1 << kBYS, "block shape");
 // F32IDX: the fp32 primary index (a.prim_f32) -- a kernel of its own: two
 // inlined primary() copies in one kernel make the compiler copy KernelArgs
 // to scratch.
+#ifdef VX_EXP_WAVE_BLOCK
+// experiment: the untiled EXT VX_EXP_WAVE_BLOCK launches one-wave workgroups (8x8 pixels)
+template <int EXT, bool TILED> constexpr bool kWaveBlockOf = EXT == VX_EXP_WAVE_BLOCK && !TILED;
+#else
+template <int EXT, bool TILED> constexpr bool kWaveBlockOf = false;
+#endif
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
-__global__ __launch_bounds__(kWG) VX_OCC_ATTR
+__global__ __launch_bounds__((kWaveBlockOf<EXT, TILED> ? 64 : kWG)) VX_OCC_ATTR
 void k_render(KernelArgs a) {
     // the shading instantiation: EXT 3/4 shade as 2; 5/6 are 1/2 with the general
     // shading block (glass in draw order, REFLECT_ALL)
@@ -1632,7 +1639,7 @@ void k_render(KernelArgs a) {
     constexpr bool kPool = EXT == 3 || EXT == 4;   // VX_FLAG_SOFT_POOL: the pooled wave pass
     constexpr bool kBrick = EXT == 4;              // VX_FLAG_SOFT_BRICK: + LDS brick staging
     constexpr bool kGeneral = EXT >= 5;            // VX_FLAG_GLASS_ORDER / VX_FLAG_REFLECT_ALL
-    __shared__ uint32_t s_px[kBY][kBX];                 // RGBA8 block staged for full-row stores
+    constexpr bool kWaveBlock = kWaveBlockOf<EXT, TILED>;
     // pooled pass: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
     // the compacted marching fragments' start (fract, cell) and lit counts
     __shared__ float4 s_sunk[kPool ? 3 * VX_MAX_SHADOW_SAMPLES : 1];
@@ -1652,10 +1659,13 @@ void k_render(KernelArgs a) {
         __syncthreads();
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int lx = ((wave % kWX) << 3) | (lane & 7);
-    const int ly = ((wave / kWX) << 3) | (lane >> 3);
+    const int lx = kWaveBlock ? (lane & 7) : (((wave % kWX) << 3) | (lane & 7));
+    const int ly = kWaveBlock ? (lane >> 3) : (((wave / kWX) << 3) | (lane >> 3));
     int ox, oy, tx0 = 0, ty0 = 0, tile_k = 0;
-    if (TILED) {
+    if (kWaveBlock) {
+        ox = blockIdx.x << 3;
+        oy = blockIdx.y << 3;
+    } else if (TILED) {
         // tiles of tile_w x tile_h pixels (multiples of the block), tile k of the
         // list at k * tile_w * tile_h in the compact output (or at its own
         // place in a w-wide frame: tile_inplace)
@@ -1888,21 +1898,11 @@ if constexpr (!kGeneral) {
 }
             }
             rgba[3] = 1.0f;
-            if (FMT == VX_PIXEL_RGBA8)
-                s_px[ly][lx] = pack_rgba8(rgba);
-            else
-                store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
+            // each wave stores its own 8x8 tile (eight 32-B row pieces per RGBA8 wave
+            // store): no block barrier, so a wave that finishes early frees its slot
+            store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
             n_px = 1;
         }
-    }
-    if (FMT == VX_PIXEL_RGBA8) {
-        // block -> framebuffer in whole rows: thread t stores pixel (t % kBX, t / kBX)
-        // of the block, so a wave writes two contiguous kBX*4-byte rows
-        __syncthreads();
-        const int sx = threadIdx.x & (kBX - 1), sy = threadIdx.x >> kBXS;
-        if (ox + sx < a.w && oy + sy < a.h)
-            reinterpret_cast<uint32_t *>(a.out)[out_index<TILED>(a, tile_k, tx0 + sx, ty0 + sy, ox + sx, oy + sy)] =
-                s_px[sy][sx];
     }
 #ifdef VX_BLOCK_TIMING
     __syncthreads();
@@ -1944,7 +1944,13 @@ if constexpr (!kGeneral) {
 // instantiation of that mode, compiled in the unit that calls it.
 template <int F, bool S, bool T, int E>
 void launch_k(const KernelArgs &a, dim3 grid, hipStream_t s) {
-    if constexpr (E >= 5) {           // the general shading modes: the integer primary index only
+    if constexpr (kWaveBlockOf<E, T>) {
+        grid = dim3((a.w + 7) / 8, (a.h + 7) / 8);
+        if (a.prim_f32)
+            hipLaunchKernelGGL((k_render<F, S, T, E, true>), grid, dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, dim3(64), 0, s, a);
+    } else if constexpr (E >= 5) {           // the general shading modes: the integer primary index only
         hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, dim3(kWG), 0, s, a);
     } else {
         if (a.prim_f32)

@@ -95,9 +95,9 @@ def render_params(name: str):
     return tuple(int(g) for g in m.groups()) if m else None
 
 
-def hot_loop_spills(lib: str, ext_max: int = 2) -> dict[tuple, tuple[int, int]]:
-    """(hot loops, spill instructions inside them) of each timed render kernel
-    (RGBA8, no stats, EXT <= ext_max).  Spill instructions: scratch_*,
+def hot_loop_spills(lib: str, ext_max: int = 6) -> dict[tuple, tuple[int, int]]:
+    """(hot loops, spill instructions inside them) of each render kernel that
+    renders frames (RGBA8, no stats, EXT <= ext_max).  Spill instructions: scratch_*,
     v_writelane, v_readlane.  Hot loops: the loops of the kernel's main body
     (before its first s_endpgm; the compiler places the rare paths after it)
     that are innermost, at most 400 instructions long, and hold a march texel
