@@ -45,6 +45,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+PMC_TAG = "r05"         # profiles/{traffic,valu}_<tag>[_c5].json: this round's rocprofv3 PMC summaries
 
 
 def parse(argv=None):
@@ -556,7 +557,7 @@ def main(argv=None):
         marched5 = rays5 - s5["shadow_rays_resolved"]
         ms5 = 1000.0 * b["wall_s"] / n5
         ach5, frac5 = roofline_of(s5["alg_bytes"], b["ev_ms"])
-        t5j = pmc_entry("traffic_r04_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
+        t5j = pmc_entry(f"traffic_{PMC_TAG}_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
         c5 = {"workload": f"C5: {c5cfg['w']}x{c5cfg['h']}, field {X5}x{Y5}x{Z5} (S-proc 3x nearest upsample), "
                           f"full quality + {c5cfg['samples']}-sample soft shadows (sun radius {args.sun_radius})",
               "ms_per_frame": round(ms5, 4), "fps": round(1000 / ms5, 2),
@@ -599,7 +600,7 @@ def main(argv=None):
         per_launch_bytes = float(stats["alg_bytes"]) / world if world > 1 else float(stats["alg_bytes"])
         kernel_ms = ev_ms if world == 1 else stats["kernel_ms"]
         achieved, frac = roofline_of(per_launch_bytes, kernel_ms) if kernel_ms else (0.0, 0.0)
-        tag = "r04" if cfg_name != "C5" else "r04_c5"
+        tag = PMC_TAG if cfg_name != "C5" else f"{PMC_TAG}_c5"
         traffic = pmc_entry(f"traffic_{tag}.json", cfg_name, cam, flags, samples) if world == 1 else None
         valu = pmc_entry(f"valu_{tag}.json", cfg_name, cam, flags, samples) if world == 1 else None
         if valu is None and not standin:
@@ -607,7 +608,7 @@ def main(argv=None):
             # every rank of N > 1 run the C3 kernel; soft shadows the C5 one)
             ref_cfg = "C5" if samples > 1 else "C3"
             c_ref = presets.CONFIGS[ref_cfg]
-            valu = pmc_entry(f"valu_r04{'_c5' if samples > 1 else ''}.json", ref_cfg, c_ref["camera"], flags,
+            valu = pmc_entry(f"valu_{PMC_TAG}{'_c5' if samples > 1 else ''}.json", ref_cfg, c_ref["camera"], flags,
                              c_ref.get("samples", 1) if samples > 1 else 1)
             if valu is not None:
                 valu = dict(valu, source=f"{valu.get('source', '')}; measured on {ref_cfg}, the same kernel "

@@ -28,7 +28,10 @@ from collections import defaultdict
 
 tag, cfg, cam, flags, samples = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
 src = sys.argv[6] if len(sys.argv) > 6 else f"gpurun_out/prof_{tag}"
-ext = 2 if samples > 1 else (1 if flags & 0x30 else 0)
+if flags & 0x3000:                                     # glass order / REFLECT_ALL: the general kernels
+    ext = 6 if samples > 1 else 5
+else:
+    ext = 2 if samples > 1 else (1 if flags & 0x30 else 0)
 KERNEL = f"k_render<1, false, false, {ext},"          # the bench's timed instantiation (RGBA8, no stats, untiled)
 os.makedirs("profiles", exist_ok=True)
 shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"profiles/{tag}_kernel_stats.csv")
