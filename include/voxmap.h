@@ -126,6 +126,10 @@ extern "C" {
  * (the launch's tail).  Identical frames. */
 #define VX_FLAG_ROWS_BOTTOM_UP 0x4000u
 #define VX_MAX_SHADOW_SAMPLES 16
+/* ABI 9: the default box cap of the primary traversal (vx_scene_desc.dist_cap
+ * = 0).  64 since round 5 (was 32): fewer steps, 2x the octant copies' memory
+ * (C3 2.3 GB, C5 20.5 GB of 288 GB); identical frames. */
+#define VX_DEFAULT_DIST_CAP 64
 
 typedef struct vx_scene vx_scene;
 
@@ -146,7 +150,8 @@ typedef struct vx_scene_desc {
     int noise_w, noise_h;       /* 0 -> 1024 x 1024 (render.js:141) */
     int X, Y, Z;                /* 0 -> 1024, 256, 32 (render.h:14-16) */
     int device;                 /* HIP device ordinal */
-    int dist_cap;               /* air-cube size cap of the primary traversal (and border width), 0 -> 32 */
+    int dist_cap;               /* air-cube size cap of the primary traversal (and border width), 0 ->
+                                   VX_DEFAULT_DIST_CAP */
     uint32_t noise_seed;        /* seed of the synthetic noise when none is given */
     int mesh_chunk;             /* ABI 8: CHUNK of the greedy mesh whose quads give the G-buffer split
                                    (voxmap.h:9, sdf.cpp:284-356); 0 -> Z; at most 255 */

@@ -102,7 +102,7 @@ def lib():
 class Oracle:
     """Scalar restatement of render.frag over one field + noise texture."""
 
-    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 32, oct_e=None, exit=False,
+    def __init__(self, field_zyx4: np.ndarray, noise_hw4: np.ndarray, cap: int = 64, oct_e=None, exit=False,
                  quad=True, chunk: int = 0):
         """exit=False: the reference's literal march (every step of
         render.frag:92-136 counted).  exit=True: the build's sun exit tables
@@ -260,7 +260,7 @@ def field_build(color_zyx: np.ndarray) -> np.ndarray:
     return out
 
 
-def field_octant(field_zyx4: np.ndarray, oct: int, cap: int = 32) -> np.ndarray:
+def field_octant(field_zyx4: np.ndarray, oct: int, cap: int = 64) -> np.ndarray:
     """(Z, Y, X) uint8: size of the all-air cube ahead of each cell for ray octant ``oct``."""
     f = np.ascontiguousarray(field_zyx4, np.uint8)
     Z, Y, X, _ = f.shape
@@ -269,7 +269,7 @@ def field_octant(field_zyx4: np.ndarray, oct: int, cap: int = 32) -> np.ndarray:
     return out
 
 
-def field_box(field_zyx4: np.ndarray, oct: int, cap: int = 32, r_cube=None) -> np.ndarray:
+def field_box(field_zyx4: np.ndarray, oct: int, cap: int = 64, r_cube=None) -> np.ndarray:
     """(Z, Y, X, 3) uint8: extents (ex, ey, ez) of the all-air box ahead of each
     cell for ray octant ``oct`` (vxo_field_box, grown from field_octant)."""
     f = np.ascontiguousarray(field_zyx4, np.uint8)

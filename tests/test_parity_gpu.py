@@ -100,9 +100,9 @@ def test_field_octant_copies_match_oracle(noise, octant):
         dev = sc.read_field(octant)
         box = sc.read_boxes(octant)
     assert np.array_equal(dev[..., :3], field[..., :3])
-    assert np.array_equal(dev[..., 3], oracle.field_octant(field, octant, 32))
+    assert np.array_equal(dev[..., 3], oracle.field_octant(field, octant))
     assert np.array_equal(box[..., 0], _vis(field[..., 2]))
-    assert np.array_equal(box[..., 1:], oracle.field_box(field, octant, 32))
+    assert np.array_equal(box[..., 1:], oracle.field_box(field, octant))
 
 
 @pytest.mark.parametrize("octant", [0, 3, 5])
@@ -118,8 +118,8 @@ def test_box_extents_full_scene_match_oracle(octant):
     with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, dims=(X, Y, Z), device=0) as sc:
         field = sc.read_field(0)
         box = sc.read_boxes(octant)
-    r = oracle.field_octant(field, octant, 32)
-    e = oracle.field_box(field, octant, 32, r_cube=r)
+    r = oracle.field_octant(field, octant)
+    e = oracle.field_box(field, octant, r_cube=r)
     assert np.array_equal(box[..., 0], _vis(field[..., 2]))
     assert np.array_equal(box[..., 1:], e)
     assert np.array_equal(e.min(axis=3), r)
@@ -410,8 +410,8 @@ def test_c5_full_frame_soft_shadows_full_quality(noise):
             oracle.lib().vxo_pixel_dir(C.addressof(fr.params), c["w"], c["h"], px, py, d)
             counts[int(d[0] < 0) | (int(d[1] < 0) << 1) | (int(d[2] < 0) << 2)] += 1
     main = int(np.argmax(counts))
-    r = oracle.field_octant(field, main, 32)
-    own = oracle.field_box(field, main, 32, r_cube=r)
+    r = oracle.field_octant(field, main)
+    own = oracle.field_box(field, main, r_cube=r)
     assert np.array_equal(own, oct_e[main])          # the device's boxes of that octant, at the C5 size
     oct_e[main] = own
     ref, ost = oracle.Oracle(field, noise, oct_e=oct_e, exit=True).render(fr.params, c["w"], c["h"], threads=16)

@@ -168,6 +168,39 @@ def main():
             bl["ideal"] += waves[waves >= 0].sum() / 64.0
         for k, v in bl.items():
             print(f"  block {k:10s} {v / max(nb, 1):9.1f} wave steps per block ({v / bl['lockstep']:.3f} of lockstep)")
+        # a global queue: every march of the sampled blocks after each fragment's
+        # sample 0 (marched in place, lockstep per wave), sorted by that sample's
+        # length, dealt 64 at a time (the best case for a grid-wide work queue)
+        gl = {"lockstep": 0.0, "queue_sorted": 0.0, "queue_unsorted": 0.0, "queue_oracle_sorted": 0.0}
+        rest, s0 = [], 0.0
+        rng2 = np.random.default_rng(3)
+        for _ in range(args.tiles // 4):
+            px0 = int(rng2.integers(0, W // 32)) * 32
+            py0 = int(rng2.integers(0, H // 8)) * 8
+            buf = np.empty((8, 32, maxrec), np.int32)
+            L.vxo_march_lengths(C.byref(o.sc), C.addressof(fr.params), W, H, px0, py0, 32, 8, buf.ctypes.data,
+                                maxrec)
+            waves = np.concatenate([buf[:, 8 * w:8 * w + 8].reshape(64, maxrec) for w in range(4)])
+            m = waves >= 0
+            if not m.any():
+                continue
+            waves = np.where(m, waves & 0xFFFF, -1)
+            gl["lockstep"] += sum(lockstep(waves[64 * w:64 * (w + 1)], args.setup) for w in range(4))
+            for w in range(4):
+                col = waves[64 * w:64 * (w + 1), 0]
+                if (col >= 0).any():
+                    s0 += col.max() + args.setup
+            for r in waves:
+                if r[0] >= 0:
+                    rest += [(int(r[0]), int(v)) for v in r[1:] if v >= 0]
+        for name, order in (("queue_sorted", sorted(rest, key=lambda kv: -kv[0])), ("queue_unsorted", rest),
+                            ("queue_oracle_sorted", sorted(rest, key=lambda kv: -kv[1]))):
+            c = s0
+            for i in range(0, len(order), 64):
+                c += max(v for _, v in order[i:i + 64]) + 2 * args.setup
+            gl[name] = c
+        for k, v in gl.items():
+            print(f"  global {k:14s} {v / max(nb, 1):9.1f} wave steps per block ({v / gl['lockstep']:.3f} of lockstep)")
     print(f"{args.config} samples={args.samples} tiles with marches={n} setup={args.setup} steps")
     for k in ("fetch_lit", "fetch_unlit", "n_lit", "n_unlit"):
         print(f"  {k:12s} {tot.pop(k, 0)}")

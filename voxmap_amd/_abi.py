@@ -37,6 +37,7 @@ FLAG_GLASS_SINGLE = 0x8000                      # diagnostics: nearest pane only
 FLAG_REFLECT_ALL = 0x2000                       # ext: every first surface mirrors the scene
 FLAG_ROWS_BOTTOM_UP = 0x4000                    # diagnostics: blocks dispatched bottom row first (same frames)
 MAX_SHADOW_SAMPLES = 16
+DEFAULT_DIST_CAP = 64                           # vx_scene_desc.dist_cap = 0 (ABI 9; was 32)
 ABI_VERSION = 9
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128

@@ -1624,14 +1624,8 @@ static_assert(kBX == 1 << kBXS && kBY == 1 << kBYS, "block shape");
 // F32IDX: the fp32 primary index (a.prim_f32) -- a kernel of its own: two
 // inlined primary() copies in one kernel make the compiler copy KernelArgs
 // to scratch.
-#ifdef VX_EXP_WAVE_BLOCK
-// experiment: the untiled EXT VX_EXP_WAVE_BLOCK launches one-wave workgroups (8x8 pixels)
-template <int EXT, bool TILED> constexpr bool kWaveBlockOf = EXT == VX_EXP_WAVE_BLOCK && !TILED;
-#else
-template <int EXT, bool TILED> constexpr bool kWaveBlockOf = false;
-#endif
 template <int FMT, bool STATS, bool TILED, int EXT, bool F32IDX>
-__global__ __launch_bounds__((kWaveBlockOf<EXT, TILED> ? 64 : kWG)) VX_OCC_ATTR
+__global__ __launch_bounds__(kWG) VX_OCC_ATTR
 void k_render(KernelArgs a) {
     // the shading instantiation: EXT 3/4 shade as 2; 5/6 are 1/2 with the general
     // shading block (glass in draw order, REFLECT_ALL)
@@ -1639,7 +1633,6 @@ void k_render(KernelArgs a) {
     constexpr bool kPool = EXT == 3 || EXT == 4;   // VX_FLAG_SOFT_POOL: the pooled wave pass
     constexpr bool kBrick = EXT == 4;              // VX_FLAG_SOFT_BRICK: + LDS brick staging
     constexpr bool kGeneral = EXT >= 5;            // VX_FLAG_GLASS_ORDER / VX_FLAG_REFLECT_ALL
-    constexpr bool kWaveBlock = kWaveBlockOf<EXT, TILED>;
     // pooled pass: the frame's sun samples (r, |r|, RN(1/|r|)) and per wave
     // the compacted marching fragments' start (fract, cell) and lit counts
     __shared__ float4 s_sunk[kPool ? 3 * VX_MAX_SHADOW_SAMPLES : 1];
@@ -1659,13 +1652,10 @@ void k_render(KernelArgs a) {
         __syncthreads();
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int lx = kWaveBlock ? (lane & 7) : (((wave % kWX) << 3) | (lane & 7));
-    const int ly = kWaveBlock ? (lane >> 3) : (((wave / kWX) << 3) | (lane >> 3));
+    const int lx = ((wave % kWX) << 3) | (lane & 7);
+    const int ly = ((wave / kWX) << 3) | (lane >> 3);
     int ox, oy, tx0 = 0, ty0 = 0, tile_k = 0;
-    if (kWaveBlock) {
-        ox = blockIdx.x << 3;
-        oy = blockIdx.y << 3;
-    } else if (TILED) {
+    if (TILED) {
         // tiles of tile_w x tile_h pixels (multiples of the block), tile k of the
         // list at k * tile_w * tile_h in the compact output (or at its own
         // place in a w-wide frame: tile_inplace)
@@ -1944,13 +1934,7 @@ if constexpr (!kGeneral) {
 // instantiation of that mode, compiled in the unit that calls it.
 template <int F, bool S, bool T, int E>
 void launch_k(const KernelArgs &a, dim3 grid, hipStream_t s) {
-    if constexpr (kWaveBlockOf<E, T>) {
-        grid = dim3((a.w + 7) / 8, (a.h + 7) / 8);
-        if (a.prim_f32)
-            hipLaunchKernelGGL((k_render<F, S, T, E, true>), grid, dim3(64), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, dim3(64), 0, s, a);
-    } else if constexpr (E >= 5) {           // the general shading modes: the integer primary index only
+    if constexpr (E >= 5) {           // the general shading modes: the integer primary index only
         hipLaunchKernelGGL((k_render<F, S, T, E, false>), grid, dim3(kWG), 0, s, a);
     } else {
         if (a.prim_f32)

@@ -96,7 +96,7 @@ class Scene:
 
     def __init__(self, *, map_path=None, map_bytes=None, map_format=_abi.FORMAT_AUTO, key=None,
                  noise_path=None, noise_bytes=None, noise_format=_abi.FORMAT_AUTO, noise_size=(1024, 1024),
-                 dims=DEFAULT_DIMS, device=0, dist_cap=32, noise_seed=0, mesh_chunk=0):
+                 dims=DEFAULT_DIMS, device=0, dist_cap=0, noise_seed=0, mesh_chunk=0):
         L = lib()
         d = _abi.SceneDesc()
         self._keep = []
