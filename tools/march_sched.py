@@ -111,7 +111,8 @@ def main():
     field = vx.field_build(grid)
     noise = scenes.real_noise()
     W, H = cfg["w"], cfg["h"]
-    fr = presets.camera_frame(cfg["camera"], W, H, flags=vx.FLAG_FULL_QUALITY, shadow_samples=args.samples,
+    up = 3.0 if cfg["scene"] == "s_up3" else 1.0
+    fr = presets.camera_frame(cfg["camera"], W, H, scale=up, flags=vx.FLAG_FULL_QUALITY, shadow_samples=args.samples,
                               sun_radius=0.03 if args.samples > 1 else 0.0)
     o = oracle.Oracle(field, noise, exit=True)
     o.hold_exit_table(fr.params)
