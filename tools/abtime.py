@@ -90,6 +90,17 @@ def main():
                 torch.cuda.synchronize()
                 if r > 0:                       # round 0 warms everything up
                     times[lab].append(e0.elapsed_time(e1) / args.frames)
+        ref = None                          # every variant's frame against the first one's
+        for lab, L, h in libs:
+            L.vx_render(h, C.byref(p), W, H, _abi.PIXEL_RGBA8, C.c_void_p(out.data_ptr()), 1,
+                        C.c_void_p(stream.cuda_stream), None)
+            torch.cuda.synchronize()
+            img = out.cpu()
+            if ref is None:
+                ref = img
+            else:
+                print(f"{args.config} flags={flags:3d} {lab:14s} {int((img != ref).sum())} bytes differ from "
+                      f"{libs[0][0]}", flush=True)
         base = None
         for lab, _, _ in libs:
             med = statistics.median(times[lab])
