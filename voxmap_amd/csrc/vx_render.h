@@ -703,36 +703,47 @@ __device__ __forceinline__ int primary(const KernelArgs &a, int oct, float d0, f
     // iv = RN(1/d) (kInf for d = 0): rcp_ranged is exact for |d| in [2^-40,
     // 2^41) -- every lane of nearly every wave (|d| = O(1)); a wave with a lane
     // outside it (a zero or tiny component) takes the IEEE division
+    // grid slabs (bounds per frame: FrameConsts::slab_lo/hi); a zero component
+    // misses unless the camera lies inside that slab
     float iv0, iv1, iv2;
+    float tlo = 0.0f, thi = kInf;
+    bool miss = false;
     {
         const unsigned lo_b = 0x2B800000u, span = 0x54000000u - 0x2B800000u;   // 2^-40, 2^41
         const bool ok = (__float_as_uint(fabsf(d0)) - lo_b) < span && (__float_as_uint(fabsf(d1)) - lo_b) < span &&
                         (__float_as_uint(fabsf(d2)) - lo_b) < span;
         if (__builtin_expect(__ballot(!ok) == 0, 1)) {
             iv0 = rcp_ranged(d0); iv1 = rcp_ranged(d1); iv2 = rcp_ranged(d2);
+            // no zero component: every slab crossing lo*iv, hi*iv is finite, and
+            // the running max / min below is the general form's (a select of one
+            // of its finite inputs; the sign of a zero t changes neither the
+            // entry point o + t*d nor tlo < thi)
+            const float a0 = F.slab_lo[0] * iv0, b0 = F.slab_hi[0] * iv0;
+            const float a1 = F.slab_lo[1] * iv1, b1 = F.slab_hi[1] * iv1;
+            const float a2 = F.slab_lo[2] * iv2, b2 = F.slab_hi[2] * iv2;
+            tlo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
+                                  __builtin_fmaxf(__builtin_fminf(a2, b2), 0.0f));
+            thi = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
+                                  __builtin_fmaxf(a2, b2));
         } else {
             iv0 = d0 != 0.0f ? 1.0f / d0 : kInf;
             iv1 = d1 != 0.0f ? 1.0f / d1 : kInf;
             iv2 = d2 != 0.0f ? 1.0f / d2 : kInf;
+#define VX_SLAB(D, IV, I)                                                     \
+            {                                                                 \
+                const float lo = F.slab_lo[I], hi = F.slab_hi[I];             \
+                const float t0 = lo * IV, t1 = hi * IV;                       \
+                const bool sw = t0 > t1, nz = D != 0.0f;                      \
+                tlo = nz ? gmax(tlo, sw ? t1 : t0) : tlo;                     \
+                thi = nz ? gmin(thi, sw ? t0 : t1) : thi;                     \
+                miss |= !nz && !(lo <= 0.0f && 0.0f < hi);                    \
+            }
+            VX_SLAB(d0, iv0, 0)
+            VX_SLAB(d1, iv1, 1)
+            VX_SLAB(d2, iv2, 2)
+#undef VX_SLAB
         }
     }
-    // grid slabs (bounds per frame: FrameConsts::slab_lo/hi); a zero component
-    // misses unless the camera lies inside that slab
-    float tlo = 0.0f, thi = kInf;
-    bool miss = false;
-#define VX_SLAB(D, IV, I)                                                     \
-    {                                                                         \
-        const float lo = F.slab_lo[I], hi = F.slab_hi[I];                     \
-        const float t0 = lo * IV, t1 = hi * IV;                               \
-        const bool sw = t0 > t1, nz = D != 0.0f;                              \
-        tlo = nz ? gmax(tlo, sw ? t1 : t0) : tlo;                             \
-        thi = nz ? gmin(thi, sw ? t0 : t1) : thi;                             \
-        miss |= !nz && !(lo <= 0.0f && 0.0f < hi);                            \
-    }
-    VX_SLAB(d0, iv0, 0)
-    VX_SLAB(d1, iv1, 1)
-    VX_SLAB(d2, iv2, 2)
-#undef VX_SLAB
     if (miss || !(tlo < thi)) return 0;
     // entry cell, camera-relative, as exact fp32 integers: floor, then clamped
     // into the grid (the former int convert + clamp; o + tlo*d is finite)
