@@ -1369,55 +1369,76 @@ __device__ __forceinline__ void shade_block(const KernelArgs &a, const Surf &g, 
 // cell is outside it).
 __device__ __forceinline__ int walk_reflect(const KernelArgs &a, int B0, int B1, int B2, float o0, float o1, float o2, float d0,
                             float d1, float d2, int c0, int c1, int c2, Surf &h, Counters &cnt) {
+    // primary()'s stepping on exact fp32 cells relative to B, h = c + hp (hp = 1
+    // on a positive axis, d = 0 counting positive), far face A = fma(s, E, h),
+    // crossing (A - o) * iv (iv = +inf for d = 0: A - o > 0, so +inf, as the
+    // integer form's explicit infinity), exit axis ties x < y < z, next h = A + s
+    // on it and med3(floor(o + te*d) + hp, h, A) on the others (= the integer
+    // form's clamp of floor(o + te*d) into [c, c+e] or [c-e, c]).  The octant
+    // copy's sentinel border (colour 0xFF) marks leaving the grid: no fetch
+    // counted, no hit, as the integer form's bounds test.
     const int oct = (d0 < 0.0f ? 1 : 0) | (d1 < 0.0f ? 2 : 0) | (d2 < 0.0f ? 4 : 0);
     const uint32_t *pp = a.prim + (size_t)oct * a.copy_texels;
-    auto inside = [&](int x, int y, int z) {
-        return (unsigned)x < (unsigned)a.X && (unsigned)y < (unsigned)a.Y && (unsigned)z < (unsigned)a.Z;
+    float iv0, iv1, iv2;
+    {
+        const unsigned lo_b = 0x2B800000u, span = 0x54000000u - 0x2B800000u;   // 2^-40, 2^41
+        const bool ok = (__float_as_uint(fabsf(d0)) - lo_b) < span && (__float_as_uint(fabsf(d1)) - lo_b) < span &&
+                        (__float_as_uint(fabsf(d2)) - lo_b) < span;
+        if (__builtin_expect(__ballot(!ok) == 0, 1)) {
+            iv0 = rcp_ranged(d0); iv1 = rcp_ranged(d1); iv2 = rcp_ranged(d2);
+        } else {
+            iv0 = d0 != 0.0f ? 1.0f / d0 : kInf;
+            iv1 = d1 != 0.0f ? 1.0f / d1 : kInf;
+            iv2 = d2 != 0.0f ? 1.0f / d2 : kInf;
+        }
+    }
+    const bool p0 = !(d0 < 0.0f), p1 = !(d1 < 0.0f), p2 = !(d2 < 0.0f);
+    const float s0 = p0 ? 1.0f : -1.0f, s1 = p1 ? 1.0f : -1.0f, s2 = p2 ? 1.0f : -1.0f;
+    const float hp0 = p0 ? 1.0f : 0.0f, hp1 = p1 ? 1.0f : 0.0f, hp2 = p2 ? 1.0f : 0.0f;
+    float h0 = (float)c0 + hp0, h1 = (float)c1 + hp1, h2 = (float)c2 + hp2;
+    // element index of the padded cell B + pad + h - hp: the x + Xp*y part as the
+    // bits of one exact fp32 fma biased by 2^23 (Xp*Yp < 2^23), z by a 24-bit
+    // multiply of the biased bits (their low 24 bits are z)
+    const float bx = (float)(B0 + a.pad) - hp0 + 8388608.0f, by = (float)(B1 + a.pad) - hp1,
+                bz = (float)(B2 + a.pad) - hp2 + 8388608.0f;
+    const float fXp = (float)a.Xp;
+    auto fetch = [&]() -> uint32_t {
+        const unsigned xy = __float_as_uint(__builtin_fmaf(h1 + by, fXp, h0 + bx)) - 0x4B000000u;
+        return pp[xy + __umul24(__float_as_uint(h2 + bz), a.XpYp)];
     };
-    auto fetch = [&](int x, int y, int z) -> uint32_t {
-        return pp[(unsigned)(x + a.pad) + (unsigned)a.Xp * (unsigned)(y + a.pad) + a.XpYp * (unsigned)(z + a.pad)];
-    };
-    const int st0 = d0 > 0.0f ? 1 : -1, st1 = d1 > 0.0f ? 1 : -1, st2 = d2 > 0.0f ? 1 : -1;
-    const float iv0 = d0 != 0.0f ? 1.0f / d0 : 0.0f, iv1 = d1 != 0.0f ? 1.0f / d1 : 0.0f,
-                iv2 = d2 != 0.0f ? 1.0f / d2 : 0.0f;
-    int x = B0 + c0, y = B1 + c1, z = B2 + c2;
-    if (!inside(x, y, z)) return 0;
-    uint32_t t = fetch(x, y, z);
+    uint32_t t = fetch();
+    if (t >= kSentinel) return 0;
     cnt.refl_fetch++;
-    int prev = t & 0xff, e0 = (int)((t >> 8) & 0xff), e1 = (int)((t >> 16) & 0xff), e2 = (int)(t >> 24);
+    int prev = t & 0xff;
+    float E0 = cvt_f32_ubyte1(t), E1 = cvt_f32_ubyte2(t), E2 = cvt_f32_ubyte3(t);
     const int cap = 4 * (a.X + a.Y + a.Z);
     for (int it = 0; it < cap; it++) {
-        const float tb0 = d0 != 0.0f ? ((float)(c0 + (st0 > 0 ? e0 + 1 : -e0)) - o0) * iv0 : kInf;
-        const float tb1 = d1 != 0.0f ? ((float)(c1 + (st1 > 0 ? e1 + 1 : -e1)) - o1) * iv1 : kInf;
-        const float tb2 = d2 != 0.0f ? ((float)(c2 + (st2 > 0 ? e2 + 1 : -e2)) - o2) * iv2 : kInf;
-        const int ax = (tb0 <= tb1 && tb0 <= tb2) ? 0 : (tb1 <= tb2 ? 1 : 2);
-        const float te = ax == 0 ? tb0 : (ax == 1 ? tb1 : tb2);
-        auto side = [&](int c, float o, float d, int e) {
-            const int v = f2i(floorf(o + te * d));
-            const int lo = d < 0.0f ? c - e : c, hi = d < 0.0f ? c : c + e;
-            return v < lo ? lo : (v > hi ? hi : v);
-        };
-        const int n0 = ax == 0 ? c0 + st0 * (e0 + 1) : side(c0, o0, d0, e0);
-        const int n1 = ax == 1 ? c1 + st1 * (e1 + 1) : side(c1, o1, d1, e1);
-        const int n2 = ax == 2 ? c2 + st2 * (e2 + 1) : side(c2, o2, d2, e2);
-        c0 = n0; c1 = n1; c2 = n2;
-        x = B0 + c0; y = B1 + c1; z = B2 + c2;
-        if (!inside(x, y, z)) return 0;
-        t = fetch(x, y, z);
+        const float A0 = __builtin_fmaf(s0, E0, h0), A1 = __builtin_fmaf(s1, E1, h1), A2 = __builtin_fmaf(s2, E2, h2);
+        const float tb0 = (A0 - o0) * iv0, tb1 = (A1 - o1) * iv1, tb2 = (A2 - o2) * iv2;
+        const float te = __builtin_fminf(__builtin_fminf(tb0, tb1), tb2);
+        const bool e0 = tb0 == te;
+        const bool e1 = !e0 && tb1 == te;
+        const int ax = e0 ? 0 : (e1 ? 1 : 2);
+        h0 = e0 ? A0 + s0 : __builtin_amdgcn_fmed3f(floorf(o0 + te * d0) + hp0, h0, A0);
+        h1 = e1 ? A1 + s1 : __builtin_amdgcn_fmed3f(floorf(o1 + te * d1) + hp1, h1, A1);
+        h2 = (!e0 && !e1) ? A2 + s2 : __builtin_amdgcn_fmed3f(floorf(o2 + te * d2) + hp2, h2, A2);
+        t = fetch();
+        if (t >= kSentinel) return 0;
         cnt.refl_fetch++;
         const int col = t & 0xff;
-        e0 = (int)((t >> 8) & 0xff); e1 = (int)((t >> 16) & 0xff); e2 = (int)(t >> 24);
+        E0 = cvt_f32_ubyte1(t); E1 = cvt_f32_ubyte2(t); E2 = cvt_f32_ubyte3(t);
         if (col != prev && col != 0) {                 // entering a meshed cell (air never is)
-            const int stp = ax == 0 ? st0 : (ax == 1 ? st1 : st2);
+            const bool pos = ax == 0 ? p0 : (ax == 1 ? p1 : p2);
+            const float r0 = h0 - hp0, r1 = h1 - hp1, r2 = h2 - hp2;   // relative cells (exact)
             h.color = col;
             h.id = col == kGlass ? 2 : 0;
-            h.nidx = 2 * ax + (stp > 0 ? 1 : 0);
-            h.c0 = (float)(x + (ax == 0 && stp < 0 ? 1 : 0));
-            h.c1 = (float)(y + (ax == 1 && stp < 0 ? 1 : 0));
-            h.c2 = (float)(z + (ax == 2 && stp < 0 ? 1 : 0));
-            h.f0 = ax == 0 ? 0.0f : (o0 + te * d0) - (float)c0;
-            h.f1 = ax == 1 ? 0.0f : (o1 + te * d1) - (float)c1;
-            h.f2 = ax == 2 ? 0.0f : (o2 + te * d2) - (float)c2;
+            h.nidx = 2 * ax + (pos ? 1 : 0);
+            h.c0 = ((float)B0 + r0) + (ax == 0 && !pos ? 1.0f : 0.0f);
+            h.c1 = ((float)B1 + r1) + (ax == 1 && !pos ? 1.0f : 0.0f);
+            h.c2 = ((float)B2 + r2) + (ax == 2 && !pos ? 1.0f : 0.0f);
+            h.f0 = ax == 0 ? 0.0f : (o0 + te * d0) - r0;
+            h.f1 = ax == 1 ? 0.0f : (o1 + te * d1) - r1;
+            h.f2 = ax == 2 ? 0.0f : (o2 + te * d2) - r2;
             return 1;
         }
         prev = col;
