@@ -31,6 +31,15 @@ ARCH = os.environ.get("VOXMAP_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall",
          "-mllvm", "-instcombine-max-copied-from-constant-users=4000", f"--offload-arch={ARCH}"]
 LIBS = ["-lz", "-lcrypto", "-lpthread", "-lrccl"]
+# per-unit code generation: the hard-shadow modes (EXT 0 / 1: the C3 frames)
+# schedule for instruction-level parallelism (LLVM's GCN max-ilp strategy):
+# identical code semantics, C3 v1 -1.5 to -1.8 %, full quality -0.6 to -0.9 %
+# (profiles/r05_ab_ilp_c3.txt, r05_ab_sched_c*.txt); the soft-shadow and
+# general units keep the default occupancy-driven schedule
+UNIT_FLAGS: dict[str, list[str]] = {
+    "vx_render_e0.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "vx_render_e1.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+}
 
 
 def hipcc() -> str:
@@ -82,7 +91,7 @@ def build(force: bool = False, verbose: bool = True, out: str | None = None, def
         if not force and os.path.exists(obj) and all(os.path.getmtime(obj) > os.path.getmtime(d)
                                                      for d in [os.path.join(CSRC, src), *hdrs]):
             continue
-        cmd = [hipcc(), *flags, "-c", "-o", obj, os.path.join(CSRC, src)]
+        cmd = [hipcc(), *flags, *UNIT_FLAGS.get(src, []), "-c", "-o", obj, os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         jobs.append((cmd, obj))
