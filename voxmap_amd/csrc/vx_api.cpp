@@ -713,6 +713,8 @@ int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts,
     const int tx = (w + ts - 1) / ts, ty = (h + ts - 1) / ts;
     for (int i = 0; i < n_tiles; i++)
         if (tile_ids[i] < 0 || tile_ids[i] >= tx * ty) return set_error(VX_EINVAL, "tile id out of range");
+    if ((unsigned long long)n_tiles * (unsigned long long)ts * (unsigned long long)ts >= (1ull << 32))
+        return set_error(VX_EINVAL, "vx_render_tiles: the compact output must hold fewer than 2^32 pixels");
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     rc = upload_ids(st, tile_ids, n_tiles, &s->d_tiles, &s->tiles_cap, s->h_tiles);
@@ -737,6 +739,8 @@ int vx_render_bands(vx_scene *s, const vx_frame_params *p, int w, int h, int ban
         if (band_ids[i] < 0 || band_ids[i] >= nb) return set_error(VX_EINVAL, "band id out of range");
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    if (!inplace && (unsigned long long)n_bands * (unsigned long long)band_rows * (unsigned long long)w >= (1ull << 32))
+        return set_error(VX_EINVAL, "vx_render_bands: the compact output must hold fewer than 2^32 pixels");
     rc = upload_ids(st, band_ids, n_bands, &s->d_bands, &s->bands_cap, s->h_bands);
     if (rc) return rc;
     TileSpec t;

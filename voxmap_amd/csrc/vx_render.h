@@ -1691,15 +1691,31 @@ void k_render(KernelArgs a) {
         // tiles of tile_w x tile_h pixels (multiples of the block), tile k of the
         // list at k * tile_w * tile_h in the compact output (or at its own
         // place in a w-wide frame: tile_inplace)
-        const int perx = a.tile_w >> kBXS, pery = a.tile_h >> kBYS;
-        const int bpt = perx * pery;
-        tile_k = blockIdx.x / bpt;
-        const int sub = blockIdx.x % bpt;
+        // (launch_render_ext: a grid of (block columns, block rows, tiles), so no
+        // integer division; a list of more than 65535 tiles takes a 1-D grid)
+        const int perx = a.tile_w >> kBXS;
+        int sx, sy;
+        if (gridDim.y > 1 || gridDim.z > 1) {
+            tile_k = blockIdx.z;
+            sx = blockIdx.x;
+            sy = blockIdx.y;
+        } else {
+            const int bpt = perx * (a.tile_h >> kBYS);
+            tile_k = blockIdx.x / bpt;
+            const int sub = blockIdx.x % bpt;
+            sx = sub % perx;
+            sy = sub / perx;
+        }
         const int tid = a.tile_ids[tile_k];
-        tx0 = (sub % perx) << kBXS;
-        ty0 = (sub / perx) << kBYS;
-        ox = (tid % a.tiles_x) * a.tile_w + tx0;
-        oy = (tid / a.tiles_x) * a.tile_h + ty0;
+        tx0 = sx << kBXS;
+        ty0 = sy << kBYS;
+        if (a.tiles_x == 1) {               // bands (vx_render_bands): one tile spans the row
+            ox = tx0;
+            oy = tid * a.tile_h + ty0;
+        } else {
+            ox = (tid % a.tiles_x) * a.tile_w + tx0;
+            oy = (tid / a.tiles_x) * a.tile_h + ty0;
+        }
     } else {
         ox = blockIdx.x << kBXS;
         // diagnostics (VX_FLAG_ROWS_BOTTOM_UP): block rows dispatched bottom row first
@@ -1707,6 +1723,9 @@ void k_render(KernelArgs a) {
     }
     const int px = ox + lx, py = oy + ly;
     const bool inframe = px < a.w && py < a.h;
+    // the tiled launch's output index, formed once: only it stays live across the
+    // shading instead of the tile's coordinates (the host keeps it below 2^32)
+    const unsigned toidx = TILED ? (unsigned)out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py) : 0u;
     const FrameConsts &F = a.fc;
     Counters cnt = {};
 #ifdef VX_BLOCK_TIMING
@@ -1922,7 +1941,7 @@ if constexpr (!kGeneral) {
             rgba[3] = 1.0f;
             // each wave stores its own 8x8 tile (eight 32-B row pieces per RGBA8 wave
             // store): no block barrier, so a wave that finishes early frees its slot
-            store_pixel<FMT>(a, out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
+            store_pixel<FMT>(a, TILED ? (size_t)toidx : out_index<TILED>(a, tile_k, tx0 + lx, ty0 + ly, px, py), rgba);
             n_px = 1;
         }
     }
@@ -1979,7 +1998,10 @@ void launch_k(const KernelArgs &a, dim3 grid, hipStream_t s) {
 template <int E>
 int launch_render_ext(const KernelArgs &a, int fmt, unsigned gx, unsigned gy, void *stream) {
     const hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(gx, gy);
+    // a tiled launch as (block columns, block rows, tiles) while the list fits the z dimension
+    const bool t3 = a.tile_ids != nullptr && a.n_tiles <= 65535;
+    const dim3 grid = t3 ? dim3((unsigned)(a.tile_w >> kBXS), (unsigned)(a.tile_h >> kBYS), (unsigned)a.n_tiles)
+                         : dim3(gx, gy);
     const bool st = a.stats != nullptr, tiled = a.tile_ids != nullptr;
     if (fmt == VX_PIXEL_RGBA32F) {
         if (st) { if (tiled) launch_k<0, true, true, E>(a, grid, s); else launch_k<0, true, false, E>(a, grid, s); }
