@@ -242,7 +242,8 @@ int vx_render(vx_scene *scene, const vx_frame_params *p, int w, int h, int pixel
 /* Render only the listed tile_size x tile_size tiles (tile t covers pixels
  * [(t % tiles_x)*ts, ...) with tiles_x = ceil(w/ts); ts a multiple of 32)
  * into a compact, tile-major device buffer: tile k of the list occupies
- * ts*ts pixels at offset k*ts*ts, row-major inside the tile. */
+ * ts*ts pixels at offset k*ts*ts, row-major inside the tile (n_tiles*ts*ts
+ * below 2^32, else VX_EINVAL). */
 int vx_render_tiles(vx_scene *scene, const vx_frame_params *p, int w, int h, int tile_size,
                     const int *tile_ids, int n_tiles, int pixel_format, void *out_device,
                     void *stream, vx_stats *stats);
@@ -275,7 +276,8 @@ int vx_detile(vx_scene *scene, int w, int h, int tile_size, const int *tile_ids,
  * [b*band_rows, (b+1)*band_rows) clipped to h; band_rows a multiple of 8.
  * inplace != 0: out is the w*h frame and each band lands at its own rows
  * (other rows untouched); inplace == 0: compact, band k of the list at
- * k*band_rows*w pixels (same row pitch w).  The multi-GPU path's unit. */
+ * k*band_rows*w pixels (same row pitch w; n_bands*band_rows*w below 2^32,
+ * else VX_EINVAL).  The multi-GPU path's unit. */
 int vx_render_bands(vx_scene *scene, const vx_frame_params *p, int w, int h, int band_rows,
                     const int *band_ids, int n_bands, int pixel_format, void *out_device,
                     int inplace, void *stream, vx_stats *stats);
