@@ -90,6 +90,10 @@ typedef struct {
 #define VXO_FLAG_GLASS_SINGLE 0x8000u
 #define VXO_FLAG_UNIT_GBUF 0x800u   /* the unit-cell G-buffer split (include/voxmap.h VX_FLAG_UNIT_GBUF) */
 #define VXO_FLAG_REFLECT_ALL 0x2000u /* ext: the first surface of every pixel mirrors the scene (as REFLECT glass) */
+/* Oracle-only diagnostic: the round-5 blend (unclamped fp32 src and dst, dst
+ * not read back from the 8-bit canvas), kept so tests can show which pixels
+ * the GL blend stage (blend_canvas) changes.  Not a kernel flag. */
+#define VXO_FLAG_BLEND_FLOAT 0x10000u
 
 typedef struct {
     uint64_t pixels, sky_px, block_px, glass_px;

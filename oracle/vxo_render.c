@@ -876,6 +876,29 @@ static void add_reflection(const shade_ctx *c, const vxo_gbuf *g, const float rd
     for (int i = 0; i < 3; i++) rgb[i] = rgb[i] + F * refl[i];
 }
 
+/* The GL blend stage.  Every draw blends SRC_ALPHA / ONE_MINUS_SRC_ALPHA
+ * (render.js:84-86) into the default framebuffer, an RGBA8 canvas (map.js:7,
+ * {alpha: false}).  For a fixed-point colour buffer GLES 3.0 §4.1.7 clamps the
+ * source, the destination and the blend factors to [0, 1] before the blend
+ * equation, and the destination is what the 8-bit buffer holds: the colour
+ * written before, stored as round(clamp(v) * 255) (the build's RGBA8 store,
+ * pack_rgba8: floor(clamp(v) * 255 + 0.5) in fp32).  An opaque fragment has
+ * alpha 1 and simply replaces the pixel.  So a pane turns the colour dst
+ * written before it into clamp(src) * a + canvas8(dst) * (1 - a), a =
+ * clamp(src.a); the next pane reads that back through canvas8 again, and the
+ * RGBA8 frame stores the last one (the fp32 frame keeps it unquantised).
+ * VXO_FLAG_BLEND_FLOAT: the round-5 fp32 blend (diagnostic). */
+static inline float canvas8(float v) { return floorf(g_clamp(v, 0.0f, 1.0f) * 255.0f + 0.5f) / 255.0f; }
+static void blend_canvas(const float src[4], float dst[3], unsigned flags) {
+    if (flags & VXO_FLAG_BLEND_FLOAT) {
+        const float a = src[3];
+        for (int i = 0; i < 3; i++) dst[i] = src[i] * a + dst[i] * (1.0f - a);
+        return;
+    }
+    const float a = g_clamp(src[3], 0.0f, 1.0f);
+    for (int i = 0; i < 3; i++) dst[i] = g_clamp(src[i], 0.0f, 1.0f) * a + canvas8(dst[i]) * (1.0f - a);
+}
+
 /* 2D mode (u_quality = 0): drawScene binds the vertex2d mesh (render.js:278,
  * 287): the footprint quads of sdf.cpp:362-401 on the plane z = 0, vert2d
  * normal byte 0 -> v_normal = (1,0,0) (render.vert:16), culled from below
@@ -931,12 +954,13 @@ static void shade_2d(const shade_ctx *c, const float d[3], float out[4], vxo_sta
     const float scatter = 1.0f - sqrtf(g_max(0.0f, f->sun_dir[2]));                 /* :168 */
     const float sp0[3] = {0.2f, 0.4f, 0.7f}, sp1[3] = {0.2f, 0.3f, 0.5f};
     const float sc0[3] = {0.7f, 0.9f, 1.0f}, sc1[3] = {1.0f, 0.3f, 0.2f};
-    const float a = 0.8f * vxo_exp2(dot3(r, n));                                    /* :247 */
+    float src[4];
+    src[3] = 0.8f * vxo_exp2(dot3(r, n));                                           /* :247 */
     for (int i = 0; i < 3; i++) {
         const float atm = g_mix(g_mix(sc0[i], sc1[i], scatter), g_mix(sp0[i], sp1[i], scatter), rz);   /* :169-171 */
-        const float src = base[i] * (0.2f * atm);                                   /* :248 */
-        out[i] = src * a + CLEAR_2D * (1.0f - a);                                   /* render.js:86 blend */
+        src[i] = base[i] * (0.2f * atm);                                            /* :248 */
     }
+    blend_canvas(src, out, f->flags);                                               /* over the clear colour */
 }
 
 /* One pixel: primary visibility, shading, glass blend (render.js:84-86
@@ -995,8 +1019,7 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
             shade_frag(c, &gl, NULL, src, rd, st);
             g_term_slot = -1;
             if (f->flags & (VXO_FLAG_REFLECT | VXO_FLAG_REFLECT_ALL)) add_reflection(c, &gl, rd, src, st);
-            const float a = src[3];
-            for (int i = 0; i < 3; i++) dst[i] = src[i] * a + dst[i] * (1.0f - a);
+            blend_canvas(src, dst, f->flags);
             depth = gl.t;
             sel.have_last = 1;
             sel.klast = gl.key;
@@ -1020,8 +1043,8 @@ static void render_pixel(const shade_ctx *c, int w, int h, int px, int py, float
         if (n == 2) shade_frag(c, &g[1], NULL, dst, NULL, st);
         else shade_frag(c, &sky, d, dst, NULL, st);
         g_term_slot = -1;
-        float a = src[3];
-        for (int i = 0; i < 3; i++) out[i] = src[i] * a + dst[i] * (1.0f - a);
+        blend_canvas(src, dst, f->flags);
+        out[0] = dst[0]; out[1] = dst[1]; out[2] = dst[2];
     }
     out[3] = 1.0f;
 }

@@ -100,3 +100,29 @@ def test_hip_reproduces_golden(built, case):
     _, ost = _exit_oracle(case.get("scene") or case["name"], field, noise).render(fr.params, w, h)
     for k, v in ost.as_dict().items():
         assert getattr(st, k) == v, k
+
+
+def test_blend_stage_decides_bright_panes(built):
+    """The GL blend stage (render.js:84-86 into the RGBA8 canvas of map.js:7;
+    oracle blend_canvas): source, destination and alpha clamped to [0, 1], the
+    destination read back as the canvas byte.  On 'blend_bright' (panes over
+    cloudy sky brighter than 1 and grazing reflections) the round-5 fp32 blend
+    (VXO_FLAG_BLEND_FLOAT) gives another frame, some pixels more than 1 LSB off;
+    every other glass pixel moves by at most 1 LSB and nothing else moves."""
+    import oracle
+    mg = _load()
+    case = next(c for c in META if c["name"] == "blend_bright")
+    field, noise, fr, w, h = mg.inputs(case)
+    O = oracle.Oracle(field, noise)
+    new, st = O.render(fr.params, w, h)
+    fr.params.flags |= mg.BLEND_FLOAT
+    old, _ = O.render(fr.params, w, h)
+    assert mg.sha(new) == case["frame_sha256"]
+    assert mg.sha(old) == case["blend_float_sha256"]
+    dq = np.abs(mg.quantise(new).astype(int) - mg.quantise(old).astype(int)).max(axis=2)
+    assert int((dq > 0).sum()) == case["blend_float_differ_rgba8"]
+    assert int((dq > 1).sum()) == case["blend_float_differ_over_1_lsb"] > 0
+    changed = np.any(new.view(np.uint32) != old.view(np.uint32), axis=2)
+    assert int(changed.sum()) <= st.glass_px          # only glass pixels blend
+    # the new frame's glass pixels are the blend of clamped values: within [0, 1]
+    assert float(new[changed][:, :3].max()) <= 1.0 and float(new[changed][:, :3].min()) >= 0.0

@@ -114,17 +114,23 @@ def test_c3_unit_split_matches_oracle(noise, flags):
 def test_s_glass_c3_default_draw_order(noise, cam, flags):
     """S-glass (panes that stack along view rays), C3, default flags: glass in
     draw order (render.js:82-91) -- the stacked pixels' chain in the main
-    kernels -- every pixel and counter against the oracle."""
+    kernels (EXT 0/1: glass_chain) with the GL blend stage -- every pixel and
+    counter against the oracle, and the same frame and counters as the
+    whole-frame general kernel (VX_FLAG_GLASS_ORDER, EXT 5) on every word."""
     import oracle
     import voxmap_amd as vx
     from voxmap_amd import presets
     field = vx.field_build(presets.scene_grid("s_glass"))
     fr = presets.camera_frame(cam, 3840, 2160, flags=flags)
+    fo = presets.camera_frame(cam, 3840, 2160, flags=flags | vx.FLAG_GLASS_ORDER)
     with _scene(vx, field, noise, (1024, 256, 32)) as sc:
         img, st = sc.render(fr, stats=True)
+        img_o, st_o = sc.render(fo, stats=True)
     ref, ost = oracle.Oracle(field, noise, exit=True).render(fr.params, 3840, 2160, threads=16)
     _compare(img, ref)
     _counters_equal(st, ost)
+    _compare(img_o, img)
+    _counters_equal(st_o, ost)
     assert st.glass_px > 100000
 
 

@@ -122,6 +122,23 @@ __device__ __forceinline__ float vexp2(float x) {
 }
 __device__ __forceinline__ float vexp(float x) { return vexp2(x * 1.44269504f); }
 
+// The GL blend stage (oracle blend_canvas).  Every draw blends SRC_ALPHA /
+// ONE_MINUS_SRC_ALPHA (render.js:84-86) into an RGBA8 canvas (map.js:7): for a
+// fixed-point buffer GLES 3.0 §4.1.7 clamps source, destination and blend
+// factors to [0, 1], and the destination is the byte the canvas holds for the
+// colour written before (pack_rgba8's floor(clamp(v) * 255 + 0.5)), read back
+// as RN(byte / 255).  A pane over dst: clamp(src) * a + canvas8(dst) * (1 - a)
+// with a = clamp(src.a); the next pane reads that back through canvas8 again.
+constexpr float kRcp255 = 1.0f / 255.0f;     // RN(1/255): div_const's reciprocal
+__device__ __forceinline__ float canvas8(float v) {
+    return div_const(floorf(gclamp(v, 0.0f, 1.0f) * 255.0f + 0.5f), 255.0f, kRcp255);   // exactly RN(q / 255)
+}
+__device__ __forceinline__ void blend_canvas(const float src[4], const float dst[3], float out[3]) {
+    const float al = gclamp(src[3], 0.0f, 1.0f);
+#pragma unroll
+    for (int i = 0; i < 3; i++) out[i] = gclamp(src[i], 0.0f, 1.0f) * al + canvas8(dst[i]) * (1.0f - al);
+}
+
 __constant__ float kPalette[22][3] = {
     {0.0f, 0.0f, 0.0f},
     {0.0431373f, 0.0627451f, 0.0745098f},
@@ -1510,9 +1527,7 @@ __device__ __forceinline__ void glass_chain(const KernelArgs &a, float d0, float
 #pragma unroll
             for (int i = 0; i < 3; i++) src[i] = src[i] + fr * refl[i];
         }
-        const float al = src[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++) dst[i] = src[i] * al + dst[i] * (1.0f - al);
+        blend_canvas(src, dst, dst);        // the pane over the canvas (render.js:84-86)
     }
 }
 
@@ -1615,14 +1630,15 @@ __device__ __forceinline__ void shade_2d(const KernelArgs &a, float d0, float d1
                (float)(0 - F.cam_cell[2]) + (0.0f - F.cam_fract[2]), r0, r1, r2);     // render.frag:154
     const float k = 2.0f * ((1.0f * r0 + 0.0f * r1) + 0.0f * r2);                  // reflect(rayDir, n)
     const float rz = sqrtf(gmax(0.0f, r2 - k * 0.0f));
-    const float al = 0.8f * vexp2((r0 * 1.0f + r1 * 0.0f) + r2 * 0.0f);
+    float src[4];
+    src[3] = 0.8f * vexp2((r0 * 1.0f + r1 * 0.0f) + r2 * 0.0f);
     const float pc[3] = {pc0, pc1, pc2};
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         const float atm = gmix(F.scatterCol[i], F.spaceCol[i], rz);
-        const float src = pc[i] * (0.2f * atm);
-        rgba[i] = src * al + kClear2d * (1.0f - al);
+        src[i] = pc[i] * (0.2f * atm);
     }
+    blend_canvas(src, rgba, rgba);          // over the clear colour in the canvas
 }
 
 // Lane = pixel, wave = 8x8 tile, workgroup = 32x8 pixels.
@@ -1896,9 +1912,7 @@ if constexpr (!kGeneral) {
 #pragma unroll
                         for (int i = 0; i < 3; i++) rgba[i] = rgba[i] + fr * refl[i];
                     }
-                    const float al = rgba[3];
-#pragma unroll
-                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+                    blend_canvas(rgba, dst, rgba);      // the nearest pane over the canvas
                 } else {
                     n_block = 1;
                 }
@@ -1930,9 +1944,7 @@ if constexpr (!kGeneral) {
                 }
                 if (glass) {
                     n_glass = 1;
-                    const float al = rgba[3];
-#pragma unroll
-                    for (int i = 0; i < 3; i++) rgba[i] = rgba[i] * al + dst[i] * (1.0f - al);
+                    blend_canvas(rgba, dst, rgba);
                 } else {
                     n_block = 1;
                 }

@@ -135,6 +135,21 @@ def single_block(dims=(64, 32, 16), at=(20, 12, 1), color=5) -> np.ndarray:
     return g
 
 
+def glass_wall(dims=(64, 64, 16)) -> np.ndarray:
+    """A glass wall (x = 36) over a ground plane with a white block behind it:
+    looking up through the wall toward the sun (hour 1.0), the panes blend over
+    cloudy sky next to the sun disc whose red exceeds 1 (render.frag:193,202:
+    clouds mix toward sunCol.r = 1.4) and, with REFLECT, mirror it at grazing
+    angles -- the case where the GL blend stage's clamps and 8-bit destination
+    (render.js:84-86, map.js:7) decide the pixel (tests/golden 'blend_bright')."""
+    X, Y, Z = dims
+    g = np.zeros((Z, Y, X), np.uint8)
+    g[0] = 2
+    g[1:Z - 1, 4:Y - 4, 36] = GLASS
+    g[1:6, 10:20, 50:56] = 20
+    return g
+
+
 def small_proc(seed: int, dims=(96, 48, 16), n_boxes=12, n_glass=3) -> np.ndarray:
     """A small S-proc-like scene that the scalar oracle renders in seconds."""
     return s_proc(seed, dims, n_boxes=n_boxes, n_glass=n_glass)
