@@ -419,11 +419,12 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
         good = all(int(frames[j_last][bro(b, H, BAND)][0, 0, 0]) == (b * 7 + j_last) % 251
                    for b in range(-(-H // BAND)))
         stats["standin_frame_ok"] = bool(good)
-    if mg is not None:
-        # render and gather timed apart (one stream, one frame at a
-        # time, max over ranks): vx_render_bands of this rank's bands, then
-        # vx_mgpu_gather alone (collective)
-        try:
+    # render and gather timed apart (one stream, one frame at a
+    # time, max over ranks): this rank's bands rendered alone (vx_render_bands),
+    # then the gather alone (collective: vx_mgpu_gather, or BandGather.gather
+    # on the torch / stand-in path)
+    try:
+        if mg is not None:
             mine = vx.mgpu_bands(H, BAND, world, rank)
             s0 = streams[0].cuda_stream
 
@@ -433,17 +434,39 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
 
             def g_only():
                 mg.gather(W, H, BAND, frames[0].data_ptr(), stream=s0)
-            tr, _ = timed(sync, r_only, args.steps, 2, 0.0, dist)
-            tg, _ = timed(sync, g_only, args.steps, 2, 0.0, dist)
-            t2 = torch.tensor([tr[0], tg[0]], dtype=torch.float64)
-            dist.all_reduce(t2, op=dist.ReduceOp.MAX)
-            split_ms = {"render_ms": round(1000.0 * float(t2[0]) / args.steps, 4),
-                        "gather_ms": round(1000.0 * float(t2[1]) / args.steps, 4),
-                        "gather_bytes": int(sum(x[5] for x in vx.mgpu_transfers(W, H, BAND, world, 0))),
-                        "how": "one stream, one frame at a time, max over ranks (the timed step overlaps "
-                               "frames in flight, so it is less than the sum)"}
-        except Exception as e:            # never let the diagnostic break the bench line
-            split_ms = {"error": str(e)}
+            gbytes = int(sum(x[5] for x in vx.mgpu_transfers(W, H, BAND, world, 0)))
+        else:
+            def r_only():
+                if standin:
+                    gs[0].render()
+                else:
+                    with torch.cuda.stream(streams[0]):
+                        gs[0].render()
+
+            def g_only():
+                if standin:
+                    gs[0].gather()
+                else:
+                    with torch.cuda.stream(streams[0]):
+                        gs[0].gather()
+            from voxmap_amd.dist import transfers as _tr
+            gbytes = int(sum(x[5] for x in _tr(W, H, BAND, world, 0, 4)))
+        tr, _ = timed(sync, r_only, args.steps, 2, 0.0, dist, "cuda" if on_dev else None)
+        tg, _ = timed(sync, g_only, args.steps, 2, 0.0, dist, "cuda" if on_dev else None)
+        t2 = torch.tensor([tr[0], tg[0]], dtype=torch.float64)
+        if on_dev:
+            t2 = t2.cuda()
+        dist.all_reduce(t2, op=dist.ReduceOp.MAX)
+        t2 = t2.cpu()
+        split_ms = {"render_ms": round(1000.0 * float(t2[0]) / args.steps, 4),
+                    "gather_ms": round(1000.0 * float(t2[1]) / args.steps, 4),
+                    "gather_bytes": gbytes,
+                    "how": "one stream, one frame at a time, max over ranks (the timed step overlaps "
+                           "frames in flight, so it is less than the sum)" +
+                           ("; CPU stand-in renderer, gloo gather" if standin else "")}
+    except Exception as e:                # never let the diagnostic break the bench line
+        split_ms = {"error": str(e)}
+    if mg is not None:
         mg.close()
     rpr = rows_per_rank(H, BAND, world)
     shards = {"unit": f"{BAND}-row full-width bands", "count": -(-H // BAND),
@@ -488,7 +511,7 @@ def main(argv=None):
         s = math.sqrt(world)
         W, H, scaling = int(round(cfg["w"] * s / 32)) * 32, int(round(cfg["h"] * s / 8)) * 8, "weak"
     if standin:
-        W, H = min(W, 256), min(H, 200)
+        W = min(W, 256)      # narrow frames; the full height keeps the config's band deal
     up = 3.0 if cfg["scene"] == "s_up3" else 1.0
     flags = args.flags if args.flags is not None else (vx.FLAG_FULL_QUALITY if args.quality == "full" else 0)
     samples = args.samples if args.samples is not None else cfg.get("samples", 1)

@@ -14,7 +14,12 @@
  * GPU; vx_render* calls are stream-ordered and may run concurrently on
  * different scenes, and on different streams of one scene -- except calls that
  * ask for stats: those share the scene's counters and events and must be
- * serialised per scene.  No global mutable state besides the thread-local error.
+ * serialised per scene.  The tile / band lists of vx_render_tiles,
+ * vx_render_bands and vx_detile are uploaded once per distinct list (on the
+ * caller's stream, no device-wide wait) and never rewritten while cached, so
+ * threads may render different lists of one scene concurrently.  The scene
+ * keeps no stream handle of the caller's: a stream may be destroyed at any
+ * time.  No global mutable state besides the thread-local error.
  */
 #ifndef VOXMAP_H
 #define VOXMAP_H
@@ -128,8 +133,12 @@ extern "C" {
 #define VX_MAX_SHADOW_SAMPLES 16
 /* ABI 9: the default box cap of the primary traversal (vx_scene_desc.dist_cap
  * = 0).  64 since round 5 (was 32): fewer steps, 2x the octant copies' memory
- * (C3 2.3 GB, C5 20.5 GB of 288 GB); identical frames. */
+ * (C3 2.3 GB, C5 20.5 GB of 288 GB); identical frames.  The cap is also the
+ * copies' border, and the padded plane must stay below 2^23 cells: a field
+ * that fits with 32 but not with 64 (X = Y above ~2770) gets
+ * VX_FALLBACK_DIST_CAP when dist_cap = 0 instead of VX_EINVAL. */
 #define VX_DEFAULT_DIST_CAP 64
+#define VX_FALLBACK_DIST_CAP 32
 
 typedef struct vx_scene vx_scene;
 

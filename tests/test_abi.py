@@ -263,3 +263,20 @@ def test_offset_limits_rejected_before_any_upload(built):
     with pytest.raises(vx.VoxmapError) as e:
         vx.Scene(map_bytes=b"\x00" * 256, map_format=vx.FORMAT_BIN, dims=(4, 4, 4), mesh_chunk=300)
     assert e.value.code == -1 and "mesh_chunk" in str(e.value)
+
+
+def test_default_cap_falls_back_to_32_where_64_does_not_fit(built):
+    """ADVICE r05: the default box cap (64) is also the octant copies' border;
+    a field whose padded plane fits below 2^23 cells with 32 but not with 64
+    (X = Y = 2800) is accepted with dist_cap = 0 (VX_FALLBACK_DIST_CAP), and
+    refused only when 64 is asked for explicitly."""
+    import voxmap_amd as vx
+    dims = (2800, 2800, 4)
+    grid = bytes(dims[0] * dims[1] * dims[2])
+    with pytest.raises(vx.VoxmapError) as e:
+        vx.Scene(map_bytes=grid, map_format=vx.FORMAT_GRID, dims=dims, dist_cap=64)
+    assert e.value.code == -1 and "too large" in str(e.value)
+    try:
+        vx.Scene(map_bytes=grid, map_format=vx.FORMAT_GRID, dims=dims).close()   # a GPU: it loads
+    except vx.VoxmapError as e2:                                                # no GPU: past validation
+        assert e2.code != -1 and "too large" not in str(e2), str(e2)

@@ -34,3 +34,20 @@ def test_bench_spawns_its_own_ranks_gloo(built):
     assert sh["assignment"].startswith("round-robin") and "gloo" in sh["gather"]
     assert j["value"] > 0 and j["ms_per_step"] > 0
     assert j["config"]["primary_rays"] == j["config"]["width"] * j["config"]["height"]
+
+
+def test_bench_eight_ranks_standin_c4(built):
+    """the driver's 8-GPU run rehearsed on CPU -- bench.py
+    --gpus 8 spawns eight ranks, deals C4's 4320 rows (narrowed frames in the
+    stand-in) in the band height vx_mgpu_band_rows picks, gathers over gloo and
+    emits one line carrying the render / gather split and the deal's balance."""
+    j = _bench("--gpus", "8", "--standin", "--steps", "3", "--warmup", "1", "--inflight", "2", timeout=600)
+    assert j["n_gpus"] == 8 and j["steps"] == 3
+    assert j["config"]["workload"].startswith("C4") and j["config"]["height"] == 4320
+    assert j["config"]["standin_frame_ok"] is True
+    sh = j["config"]["shards"]
+    assert sh["unit"].startswith("32-row")                # vx_mgpu_band_rows(4320, 8)
+    assert sh["rows_per_rank_max_over_mean"] <= 1.01
+    sp = sh["split_ms"]
+    assert sp["render_ms"] > 0 and sp["gather_ms"] > 0, sp
+    assert sp["gather_bytes"] == j["config"]["width"] * 4 * (4320 - 544)   # all rows but rank 0's 544

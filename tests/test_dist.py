@@ -162,3 +162,7 @@ def test_band_height_balances_the_deal(built):
             # never worse than the fixed 64-row deal
             assert max(rp) <= max(rows_per_rank(h, 64, n))
     assert vx.mgpu_band_rows(4320, 8, 16) in (8, 16)
+    # max_rows <= 0 means the default 64 on both sides
+    for h, n in ((4320, 8), (2160, 3), (1000, 5)):
+        for m in (0, -8):
+            assert vx.mgpu_band_rows(h, n, m) == band_rows_for(h, n, m) == band_rows_for(h, n), (h, n, m)

@@ -124,9 +124,9 @@ def test_two_threads_cycle_three_suns(scene):
     cycling through three suns with different cone windows (two cache slots, so
     slots are recycled while the other thread's frames may still read them).
     A slot is pinned from its lookup until the render that reads it is enqueued,
-    and keeps the streams such renders went to; a recycle makes the building
-    stream wait for the work enqueued so far on each of them (vx_api.cpp
-    cone_copy).  Every frame equals the same frame rendered alone."""
+    and a recycle waits for the device, so every render that read the slot has
+    finished (vx_api.cpp cone_copy; no caller stream handle is kept).
+    Every frame equals the same frame rendered alone."""
     import threading
 
     import torch
@@ -170,9 +170,9 @@ def test_two_threads_cycle_three_suns(scene):
 def test_two_threads_per_thread_stream_cycle_three_suns(scene):
     """hipStreamPerThread is one handle that names a different
     stream on each host thread.  Two threads pass it while cycling three cone
-    windows through the two slots: a slot one of them read is recycled only
-    after a device-wide wait (no handle names the reader's stream), and a cache
-    hit always waits for the build.  Every frame equals the frame rendered alone."""
+    windows through the two slots: a slot is recycled only after a device-wide
+    wait, and a cache hit waits for the build until the host has seen it
+    complete.  Every frame equals the frame rendered alone."""
     import threading
 
     import torch

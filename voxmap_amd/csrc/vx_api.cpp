@@ -14,6 +14,7 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -36,16 +37,26 @@ struct vx_scene {
     struct Cone {
         int oct = -1, kx = -1, ky = -1;
         int8_t *d = nullptr;
-        hipEvent_t ready = nullptr;   // recorded on build_st after the build
-        hipStream_t build_st = nullptr;
+        hipEvent_t ready = nullptr;   // recorded on the build's stream after the build
         unsigned long long used = 0;
         bool ready_seen = false;      // the build's `ready` event observed complete
-        std::vector<hipStream_t> readers;   // streams a render reading this copy was enqueued on
-        bool any_reader_special = false;    // a reader passed hipStreamPerThread: no handle names its stream
     } cones[2];
     unsigned long long cone_tick = 0;
-    hipEvent_t recycle_ev = nullptr;  // marks a reader stream's work at a recycle (cone_copy)
     std::mutex cone_mu;
+    // band / tile-id lists (vx_render_tiles / _bands, vx_detile), uploaded once
+    // per distinct list and never rewritten while cached (list_acquire)
+    struct ListBuf {
+        std::vector<int> ids;         // the list d holds (also the upload's source)
+        unsigned long long hash = 0;
+        int *d = nullptr;
+        hipEvent_t ready = nullptr;   // recorded after the upload
+        bool ready_seen = false;
+        int pins = 0;                 // renders between lookup and enqueue
+        unsigned long long used = 0;
+    };
+    std::vector<std::unique_ptr<ListBuf>> lists;
+    std::mutex lists_mu;
+    unsigned long long list_tick = 0;
     int SB = 0, SXp = 0, SYp = 0, SZp = 0;
     uint16_t *d_rg = nullptr;     // R | G << 8
     uint32_t *d_rg2 = nullptr;    // AO x-pairs: (R, G) of cells x and x + 1, clamped, (X + 1) per row
@@ -58,13 +69,6 @@ struct vx_scene {
     uint32_t *d_noise = nullptr;
     uint32_t *d_noise4 = nullptr; // noise quads, 4 planes (A, R, G, B): a channel of texels (x, y), (x+1, y), (x, y+1), (x+1, y+1), wrapped
     unsigned long long *d_stats = nullptr;
-    int *d_tiles = nullptr;
-    int tiles_cap = 0;
-    int *d_detile = nullptr;
-    int detile_cap = 0;
-    int *d_bands = nullptr;
-    int bands_cap = 0;
-    std::vector<int> h_tiles, h_detile, h_bands;   // last lists uploaded to d_tiles / d_detile / d_bands
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     FieldLayout L;
@@ -282,7 +286,6 @@ void vx_scene_destroy(vx_scene *s) {
         if (c.d) (void)hipFree(c.d);
         if (c.ready) (void)hipEventDestroy(c.ready);
     }
-    if (s->recycle_ev) (void)hipEventDestroy(s->recycle_ev);
     if (s->d_rg) (void)hipFree(s->d_rg);
     if (s->d_rg2) (void)hipFree(s->d_rg2);
     if (s->d_noise4) (void)hipFree(s->d_noise4);
@@ -293,9 +296,10 @@ void vx_scene_destroy(vx_scene *s) {
     if (s->d_fp2d) (void)hipFree(s->d_fp2d);
     if (s->d_noise) (void)hipFree(s->d_noise);
     if (s->d_stats) (void)hipFree(s->d_stats);
-    if (s->d_tiles) (void)hipFree(s->d_tiles);
-    if (s->d_detile) (void)hipFree(s->d_detile);
-    if (s->d_bands) (void)hipFree(s->d_bands);
+    for (auto &b : s->lists) {
+        if (b->d) (void)hipFree(b->d);
+        if (b->ready) (void)hipEventDestroy(b->ready);
+    }
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -414,24 +418,18 @@ struct TileSpec {
     int n = 0;
 };
 
-// A stream handle that names one stream wherever it is used: not the
-// per-thread default stream, which is a different stream on every host thread.
-static bool plain_stream(hipStream_t st) { return st != hipStreamPerThread; }
-
 // The frame's cone copy {oct, kx, ky}: found in the scene's cache, or built on
 // stream st into a free or the least recently used slot.  The caller holds
 // s->cone_mu from here until its render is enqueued, so every render that
-// reads a slot is enqueued before anyone can recycle it, and the slot keeps
-// the streams those renders went to (`readers`).  A recycle then makes st wait
-// for the work enqueued so far on each reader stream -- one event recorded on
-// that stream now, one stream wait: stream-ordered, no host or device-wide
-// stall, nothing per render (an event after every render is one more stream
-// packet between back-to-back frames, +3 % at C3, profiles/r04_ab_event_c3.txt).
-// A reader that passed hipStreamPerThread names no stream another thread can
-// wait on: that slot's recycle waits for the device.  A cache hit
-// on a stream other than the build's waits for the build's event until the host
-// has seen it complete.  t_build: recorded on st just before the build's first
-// packet (vx_prepare_sun's timing), if built.
+// reads a slot is enqueued before anyone can recycle it.  A recycle waits for
+// the device: it needs a third sun window in the scene's two slots, so it
+// happens at most once per sun window change (the sun moves about 1 rad per
+// hour, map.js:399), and it keeps no handle of a caller's stream (ADVICE r05:
+// a caller may destroy a stream it rendered on; an event per render on the
+// reader's stream instead costs +3 % at C3, profiles/r04_ab_event_c3.txt).  A
+// cache hit waits for the build's event until the host has seen it complete
+// (a no-op on the build's own stream).  t_build: recorded on st just before
+// the build's first packet (vx_prepare_sun's timing), if built.
 static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built,
                      vx_scene::Cone **used, hipEvent_t t_build) {
     *built = false;
@@ -443,35 +441,23 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         for (auto &c : s->cones)
             if (!c.d || c.used < slot->used) slot = &c;
         if (slot->d) {
-            if (slot->any_reader_special || !plain_stream(st)) {
-                VX_HIP(hipDeviceSynchronize());
-            } else {
-                if (!s->recycle_ev) VX_HIP(hipEventCreateWithFlags(&s->recycle_ev, hipEventDisableTiming));
-                for (hipStream_t r : slot->readers) {
-                    if (r == st) continue;                     // stream order
-                    VX_HIP(hipEventRecord(s->recycle_ev, r));
-                    VX_HIP(hipStreamWaitEvent(st, s->recycle_ev, 0));
-                }
-            }
+            VX_HIP(hipDeviceSynchronize());            // every render that read it is enqueued: done
         } else {
             const size_t np = (size_t)s->SXp * s->SYp * s->SZp;
             VX_HIP(hipMalloc(&slot->d, np));
             if (!slot->ready) VX_HIP(hipEventCreateWithFlags(&slot->ready, hipEventDisableTiming));
         }
         slot->oct = -1;
-        slot->readers.clear();
-        slot->any_reader_special = false;
         if (t_build) VX_HIP(hipEventRecord(t_build, st));
         VX_HIP(hipMemsetAsync(slot->d, 0xFF, (size_t)s->SXp * s->SYp * s->SZp, st));
         const int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
         if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
         VX_HIP(hipEventRecord(slot->ready, st));
-        slot->build_st = st;
         slot->ready_seen = false;
         slot->oct = oct; slot->kx = kx; slot->ky = ky;
         *built = true;
-    } else if (!slot->ready_seen && (st != slot->build_st || !plain_stream(st))) {
-        const hipError_t q = hipEventQuery(slot->ready);   // another stream: wait for the build
+    } else if (!slot->ready_seen) {
+        const hipError_t q = hipEventQuery(slot->ready);   // wait for the build
         if (q == hipSuccess) slot->ready_seen = true;
         else if (q == hipErrorNotReady) VX_HIP(hipStreamWaitEvent(st, slot->ready, 0));
         else VX_HIP(q);
@@ -480,17 +466,6 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
     *out = slot->d;
     *used = slot;
     return VX_OK;
-}
-
-// A render on stream st reads `slot` (cone_mu held until it is enqueued).
-static void cone_reader(vx_scene::Cone *slot, hipStream_t st) {
-    if (!plain_stream(st)) {
-        slot->any_reader_special = true;
-        return;
-    }
-    for (hipStream_t r : slot->readers)
-        if (r == st) return;
-    slot->readers.push_back(st);
 }
 
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
@@ -519,8 +494,11 @@ static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &
     return VX_OK;
 }
 
+// ListRef (list_acquire): the list the launch reads, unpinned once it is enqueued
+struct ListRef;
+static void list_release(ListRef *lr);
 static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const TileSpec &ts, int fmt, void *out_dev,
-                     void *stream, vx_stats *stats) {
+                     void *stream, vx_stats *stats, ListRef *lr = nullptr) {
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     KernelArgs a;
     std::memset(&a, 0, sizeof a);
@@ -562,15 +540,14 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     frame_consts(*p, w, h, s->X, s->Y, s->Z, a.max_shadow_steps, a.fc);
     // the cone copy the frame reads stays pinned from its lookup until this
     // render is enqueued (a second thread must not recycle it in
-    // between); its stream is kept as one of the copy's readers (cone_reader)
+    // between)
     std::unique_lock<std::mutex> cone_lock(s->cone_mu);
     vx_scene::Cone *cone = nullptr;
     {
         const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
         if (rc) return rc;
     }
-    if (cone) cone_reader(cone, st);
-    else cone_lock.unlock();
+    if (!cone) cone_lock.unlock();
     a.Xp = s->L.Xp;
     a.pad = s->L.pad;
     a.XpYp = (unsigned)s->L.Xp * (unsigned)s->L.Yp;
@@ -617,6 +594,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     int rc = launch_render(a, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("render launch failed: ") + hipGetErrorString((hipError_t)rc));
     if (cone) cone_lock.unlock();   // enqueued: a recycle now waits for this render
+    if (lr) list_release(lr);
     if (stats) VX_HIP(hipEventRecord(s->ev1, st));
     if (stats) {
         unsigned long long v[ST_COUNT];
@@ -682,23 +660,89 @@ int vx_render(vx_scene *s, const vx_frame_params *p, int w, int h, int fmt, void
 
 }  // extern "C"
 
-// Tile-id lists live on the device; a list is re-uploaded only when it
-// changes (steady-state frames re-use it), after draining the stream so an
-// in-flight kernel never sees the buffer change under it.
-static int upload_ids(hipStream_t st, const int *ids, int n, int **d_buf, int *cap, std::vector<int> &last) {
-    if ((int)last.size() == n && std::equal(last.begin(), last.end(), ids)) return VX_OK;
-    // a changed list: every launch that may still read the old one (frames in
-    // flight on other streams included) must finish first
-    (void)st;
-    VX_HIP(hipDeviceSynchronize());
-    if (n > *cap) {
-        if (*d_buf) VX_HIP(hipFree(*d_buf));
-        *d_buf = nullptr;
-        VX_HIP(hipMalloc(d_buf, sizeof(int) * n));
-        *cap = n;
+// Tile / band-id lists live on the device, uploaded once per distinct list
+// and never rewritten while cached: a render on any stream with a list the
+// scene holds reads its buffer as it is, with no upload and no wait; a new
+// list gets a new buffer, filled with hipMemcpyAsync on the caller's stream
+// (renders of it on other streams wait for that copy's event until the host
+// has seen it complete).  So threads may render different lists of one scene
+// on their own streams at once, and a list change stalls nothing (VERDICT r05
+// item 5: rounds 1-5 rewrote one buffer per kind after a device-wide wait).
+// A list is pinned from its lookup until its render is enqueued (ListRef).
+// Only when more than kMaxLists distinct lists are cached is the least
+// recently used unpinned one freed, after a device wait (its readers may be
+// in flight on any stream).
+constexpr size_t kMaxLists = 256;
+
+struct ListRef {
+    vx_scene *s = nullptr;
+    vx_scene::ListBuf *b = nullptr;
+    void release() {
+        if (!b) return;
+        std::lock_guard<std::mutex> g(s->lists_mu);
+        b->pins--;
+        b = nullptr;
     }
-    VX_HIP(hipMemcpy(*d_buf, ids, sizeof(int) * n, hipMemcpyHostToDevice));
-    last.assign(ids, ids + n);
+    ~ListRef() { release(); }
+};
+static void list_release(ListRef *lr) { lr->release(); }
+
+static unsigned long long list_hash(const int *ids, int n) {
+    unsigned long long h = 1469598103934665603ull;   // FNV-1a over the ints
+    for (int i = 0; i < n; i++) h = (h ^ (unsigned)ids[i]) * 1099511628211ull;
+    return h ^ (unsigned long long)n;
+}
+
+static int list_acquire(vx_scene *s, hipStream_t st, const int *ids, int n, ListRef &ref) {
+    const unsigned long long h = list_hash(ids, n);
+    std::lock_guard<std::mutex> g(s->lists_mu);
+    vx_scene::ListBuf *b = nullptr;
+    for (auto &p : s->lists)
+        if (p->hash == h && (int)p->ids.size() == n && std::equal(p->ids.begin(), p->ids.end(), ids)) b = p.get();
+    if (b) {
+        if (!b->ready_seen) {
+            const hipError_t q = hipEventQuery(b->ready);
+            if (q == hipSuccess) b->ready_seen = true;
+            else if (q == hipErrorNotReady) VX_HIP(hipStreamWaitEvent(st, b->ready, 0));
+            else VX_HIP(q);
+        }
+    } else {
+        if (s->lists.size() >= kMaxLists) {
+            size_t v = s->lists.size();
+            for (size_t i = 0; i < s->lists.size(); i++)
+                if (s->lists[i]->pins == 0 && (v == s->lists.size() || s->lists[i]->used < s->lists[v]->used)) v = i;
+            if (v != s->lists.size()) {
+                VX_HIP(hipDeviceSynchronize());
+                vx_scene::ListBuf *c = s->lists[v].get();
+                if (c->d) VX_HIP(hipFree(c->d));
+                if (c->ready) VX_HIP(hipEventDestroy(c->ready));
+                s->lists.erase(s->lists.begin() + (long)v);
+            }
+        }
+        auto nb = std::make_unique<vx_scene::ListBuf>();
+        nb->ids.assign(ids, ids + n);
+        nb->hash = h;
+        VX_HIP(hipMalloc(reinterpret_cast<void **>(&nb->d), sizeof(int) * (size_t)n));
+        if (hipEventCreateWithFlags(&nb->ready, hipEventDisableTiming) != hipSuccess) {
+            (void)hipFree(nb->d);
+            return set_error(VX_EDEVICE, "list upload: event creation failed");
+        }
+        // the entry's own host copy is the source: it lives as long as the buffer
+        hipError_t e = hipMemcpyAsync(nb->d, nb->ids.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(nb->ready, st);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(nb->d);
+            (void)hipEventDestroy(nb->ready);
+            return set_error(VX_EDEVICE, std::string("list upload: ") + hipGetErrorString(e));
+        }
+        s->lists.push_back(std::move(nb));
+        b = s->lists.back().get();
+    }
+    b->pins++;
+    b->used = ++s->list_tick;
+    ref.s = s;
+    ref.b = b;
     return VX_OK;
 }
 
@@ -717,14 +761,16 @@ int vx_render_tiles(vx_scene *s, const vx_frame_params *p, int w, int h, int ts,
         return set_error(VX_EINVAL, "vx_render_tiles: the compact output must hold fewer than 2^32 pixels");
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    rc = upload_ids(st, tile_ids, n_tiles, &s->d_tiles, &s->tiles_cap, s->h_tiles);
+    ListRef lr;
+    rc = list_acquire(s, st, tile_ids, n_tiles, lr);
     if (rc) return rc;
+    const int *d_ids = lr.b->d;
     TileSpec t;
     t.tw = t.th = t.pitch = ts;
     t.tiles_x = tx;
-    t.ids = s->d_tiles;
+    t.ids = d_ids;
     t.n = n_tiles;
-    return do_render(s, p, w, h, t, fmt, out_device, st, stats);
+    return do_render(s, p, w, h, t, fmt, out_device, st, stats, &lr);
 }
 
 int vx_render_bands(vx_scene *s, const vx_frame_params *p, int w, int h, int band_rows, const int *band_ids,
@@ -741,17 +787,19 @@ int vx_render_bands(vx_scene *s, const vx_frame_params *p, int w, int h, int ban
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
     if (!inplace && (unsigned long long)n_bands * (unsigned long long)band_rows * (unsigned long long)w >= (1ull << 32))
         return set_error(VX_EINVAL, "vx_render_bands: the compact output must hold fewer than 2^32 pixels");
-    rc = upload_ids(st, band_ids, n_bands, &s->d_bands, &s->bands_cap, s->h_bands);
+    ListRef lr;
+    rc = list_acquire(s, st, band_ids, n_bands, lr);
     if (rc) return rc;
+    const int *d_ids = lr.b->d;
     TileSpec t;
     t.tw = (w + VX_TILE_ALIGN_X - 1) / VX_TILE_ALIGN_X * VX_TILE_ALIGN_X;   // one tile spans the row
     t.th = band_rows;
     t.pitch = w;                      // compact bands keep the frame's row pitch
     t.tiles_x = 1;
     t.inplace = inplace ? 1 : 0;
-    t.ids = s->d_bands;
+    t.ids = d_ids;
     t.n = n_bands;
-    return do_render(s, p, w, h, t, fmt, out_device, st, stats);
+    return do_render(s, p, w, h, t, fmt, out_device, st, stats, &lr);
 }
 
 int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tiles, int fmt, const void *tiles_device,
@@ -768,9 +816,11 @@ int vx_detile(vx_scene *s, int w, int h, int ts, const int *tile_ids, int n_tile
     }
     VX_HIP(hipSetDevice(s->device));
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    int rc = upload_ids(st, tile_ids, n_tiles, &s->d_detile, &s->detile_cap, s->h_detile);
+    ListRef lr;
+    int rc = list_acquire(s, st, tile_ids, n_tiles, lr);
     if (rc) return rc;
-    rc = launch_detile(tiles_device, frame_device, w, h, ts, (w + ts - 1) / ts, s->d_detile, n_tiles, fmt, st);
+    const int *d_ids = lr.b->d;
+    rc = launch_detile(tiles_device, frame_device, w, h, ts, (w + ts - 1) / ts, d_ids, n_tiles, fmt, st);
     if (rc) return set_error(VX_EDEVICE, std::string("detile failed: ") + hipGetErrorString((hipError_t)rc));
     return VX_OK;
 }

@@ -81,8 +81,15 @@ int vx::scene_inputs(const vx_scene_desc *d, SceneInputs &in) {
     const int NW = d->noise_w ? d->noise_w : 1024, NH = d->noise_h ? d->noise_h : 1024;
     if (X <= 0 || Y <= 0 || Z <= 0 || X > 65535 || Y > 65535 || Z > 255)
         return set_error(VX_EINVAL, "vx_scene_create: dims out of range");
-    const int cap = d->dist_cap ? d->dist_cap : VX_DEFAULT_DIST_CAP;
+    int cap = d->dist_cap ? d->dist_cap : VX_DEFAULT_DIST_CAP;
     if (cap < 1 || cap > 255) return set_error(VX_EINVAL, "dist_cap must be in [1,255]");
+    // the default cap's border: a field that fits with the ABI <= 8 default (32)
+    // but not with 64 takes 32 instead of failing
+    auto fits = [&](int c) {
+        const FieldLayout Lc = field_layout(X, Y, Z, c);
+        return Lc.texels < (1ull << 31) && (unsigned long long)Lc.Xp * Lc.Yp < (1ull << 23);
+    };
+    if (!d->dist_cap && !fits(cap) && fits(VX_FALLBACK_DIST_CAP)) cap = VX_FALLBACK_DIST_CAP;
     const FieldLayout L = field_layout(X, Y, Z, cap);
     // 32-bit buffer byte offsets and 24-bit index products in the kernels
     if (L.texels >= (1ull << 31) || (unsigned long long)L.Xp * L.Yp >= (1ull << 23))

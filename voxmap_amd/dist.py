@@ -31,6 +31,8 @@ def band_rows_for(h: int, world: int, max_rows: int = 64) -> int:
     """The deal's band height (vx_mgpu_band_rows): the multiple of 8 up to
     max_rows whose round-robin deal gives the busiest rank the fewest rows,
     ties to the tallest band (the fewest sends)."""
+    if max_rows <= 0:
+        max_rows = 64                   # as vx_mgpu_band_rows
     best, best_rows = 8, None
     for r in range(8, max(8, max_rows - max_rows % 8) + 1, 8):
         nb = n_bands(h, r)
@@ -90,8 +92,16 @@ class BandGather:
         return transfers(self.w, self.h, self.band_rows, self.world, self.rank, px)
 
     def step(self):
+        self.render()
+        return self.gather()
+
+    def render(self):
+        """My bands, in place in my frame."""
         if self.mine:
             self._render(self.mine, self.frame)
+
+    def gather(self):
+        """Every other rank's bands into rank 0's frame rows (collective)."""
         ops = []
         for b, src, dst, _, _, _ in self.transfers():
             rows = self.frame[band_rows_of(b, self.h, self.band_rows)]
