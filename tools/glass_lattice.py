@@ -67,11 +67,17 @@ def main():
                     for tag, fl in (("order", 48), ("single", 48 | vx.FLAG_GLASS_SINGLE)):
                         fr = presets.camera_frame(cam, W, H, flags=fl)
                         sc.prepare_sun(fr)
-                        ms, glass = [], 0
-                        for _ in range(args.frames):
-                            s = sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True)
-                            ms.append(s.kernel_ms)
-                            glass = s.glass_px
+                        glass = sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True).glass_px
+                        sid = torch.cuda.current_stream().cuda_stream
+                        ms = []
+                        for _ in range(7):          # median of 7 blocks of `frames` timed (non-STATS) launches
+                            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            e0.record()
+                            for _ in range(args.frames):
+                                sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sid)
+                            e1.record()
+                            torch.cuda.synchronize()
+                            ms.append(e0.elapsed_time(e1) / args.frames)
                         res[f"{name}:{cam}:{tag}"] = {"ms": round(statistics.median(ms), 4), "glass_px": int(glass)}
                         print(name, cam, tag, res[f"{name}:{cam}:{tag}"], flush=True)
     if args.out:
