@@ -74,9 +74,12 @@ def parse(argv=None):
     ap.add_argument("--flags", type=int, default=None, help="VX_FLAG_* bits overriding --quality (diagnostics)")
     ap.add_argument("--samples", type=int, default=None, help="soft-shadow samples (default: 16 for C5, else 1)")
     ap.add_argument("--sun-radius", type=float, default=0.03)
-    ap.add_argument("--gather", choices=["native", "torch"], default="native",
+    ap.add_argument("--gather", choices=["native", "torch", "gloo"], default="native",
                     help="N > 1: native = vx_mgpu_render (RCCL from C++); torch = the same bands over "
-                         "torch.distributed 'nccl'")
+                         "torch.distributed 'nccl'; gloo = a rehearsal on ONE GPU (RCCL refuses two ranks on "
+                         "one device): every rank renders its bands on the GPU (VOXMAP_BENCH_DEVICE, default "
+                         "LOCAL_RANK), the bands travel over gloo through host memory, and rank 0 checks the "
+                         "gathered frame against a whole-frame vx_render (config.gather_frame_ok); not a timing")
     ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -332,7 +335,8 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
     frames = [torch.empty((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(K)]
     group = None
     gather = args.gather
-    if standin:
+    gloo = gather == "gloo" and not standin
+    if standin or gloo:
         gather = "torch"
     elif gather == "native":
         uid = [vx.mgpu_unique_id() if rank == 0 else None]
@@ -364,16 +368,24 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
                 def rb(ids, fr, j=j):                  # stand-in renderer: each band filled from its id
                     for b in ids:
                         fr[band_rows_of(b, H, BAND)] = (b * 7 + j) % 251
+            elif gloo:
+                def rb(ids, fr, j=j, sj=streams[j]):  # render on the GPU, bands to host for gloo
+                    scene.render_bands(frame, BAND, ids, frames[j].data_ptr(), inplace=True, stream=sj.cuda_stream)
+                    sj.synchronize()
+                    for b in ids:
+                        r = band_rows_of(b, H, BAND)
+                        fr[r] = frames[j][r].cpu()
             else:
                 def rb(ids, fr, sj=streams[j].cuda_stream):
                     scene.render_bands(frame, BAND, ids, fr.data_ptr(), inplace=True, stream=sj)
-            g = BandGather(dist, W, H, BAND, 4, torch.uint8, dev, rb, group=group)
-            g.frame = frames[j]
+            g = BandGather(dist, W, H, BAND, 4, torch.uint8, "cpu" if gloo else dev, rb, group=group)
+            if not gloo:
+                g.frame = frames[j]
             gs.append(g)
 
         def mk(j):
             def f():
-                if standin:
+                if standin or gloo:
                     gs[j].step()
                 else:
                     with torch.cuda.stream(streams[j]):
@@ -390,10 +402,11 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
                                     stream=streams[0].cuda_stream, stats=True).as_dict()
         gather_desc = ("torch.distributed batch_isend_irecv into rank 0's frame rows" +
                        (" (fallback: vx_mgpu_create failed)" if group is not None else "") +
-                       (" (gloo, CPU stand-in renderer)" if standin else " (RCCL)"))
+                       (" (gloo, CPU stand-in renderer)" if standin else
+                        " (gloo through host memory: one-GPU rehearsal, not a timing)" if gloo else " (RCCL)"))
     keys = [k for k in st.keys() if k != "kernel_ms"]
     vec = torch.tensor([float(st[k]) for k in keys], dtype=torch.float64)
-    on_dev = gather == "torch" and not standin
+    on_dev = gather == "torch" and not standin and not gloo
     if on_dev:
         vec = vec.cuda()
     dist.all_reduce(vec)
@@ -412,6 +425,14 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)             # per block, the slowest rank
     med, blocks = block_summary([float(v) for v in tt.cpu().tolist()], args.steps)
     wall = med * args.steps / 1000.0
+    if gloo:
+        # the rehearsal's check: rank 0's gathered frame == one whole-frame render
+        j_last = (n[0] - 1) % K
+        if rank == 0:
+            full = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+            scene.render_device(frame, full.data_ptr(), pixel_format=vx.PIXEL_RGBA8)
+            torch.cuda.synchronize()
+            stats["gather_frame_ok"] = bool(torch.equal(full.cpu(), gs[j_last].frame))
     if rank == 0 and standin:
         # the gathered frame must hold every band's stand-in value
         from voxmap_amd.dist import band_rows_of as bro
@@ -437,14 +458,14 @@ def multi_rank(args, torch, dist, vx, scene, frame, W, H, K, rank, world, local,
             gbytes = int(sum(x[5] for x in vx.mgpu_transfers(W, H, BAND, world, 0)))
         else:
             def r_only():
-                if standin:
+                if standin or gloo:
                     gs[0].render()
                 else:
                     with torch.cuda.stream(streams[0]):
                         gs[0].render()
 
             def g_only():
-                if standin:
+                if standin or gloo:
                     gs[0].gather()
                 else:
                     with torch.cuda.stream(streams[0]):
@@ -487,6 +508,8 @@ def main(argv=None):
     world = max(int(os.environ.get("WORLD_SIZE", "1")), 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gather == "gloo":                  # one-GPU rehearsal: every rank on this device
+        local = int(os.environ.get("VOXMAP_BENCH_DEVICE", str(local)))
     standin = args.standin
     if world > 1:
         # native gather: RCCL lives in libvoxmap_hip.so; torch.distributed (gloo) only
@@ -715,6 +738,8 @@ def main(argv=None):
         }
         if standin:
             result["config"]["standin_frame_ok"] = stats.get("standin_frame_ok")
+        if "gather_frame_ok" in stats:
+            result["config"]["gather_frame_ok"] = stats["gather_frame_ok"]
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(scene, noise, frame, W, H, args.cpu_seconds)
     if scene is not None:

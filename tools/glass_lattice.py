@@ -68,14 +68,15 @@ def main():
                         fr = presets.camera_frame(cam, W, H, flags=fl)
                         sc.prepare_sun(fr)
                         glass = sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True).glass_px
-                        sid = torch.cuda.current_stream().cuda_stream
+                        st = torch.cuda.Stream()          # events and launches on one non-default stream
                         ms = []
                         for _ in range(7):          # median of 7 blocks of `frames` timed (non-STATS) launches
                             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                            e0.record()
+                            e0.record(st)
                             for _ in range(args.frames):
-                                sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stream=sid)
-                            e1.record()
+                                sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8,
+                                                 stream=st.cuda_stream)
+                            e1.record(st)
                             torch.cuda.synchronize()
                             ms.append(e0.elapsed_time(e1) / args.frames)
                         res[f"{name}:{cam}:{tag}"] = {"ms": round(statistics.median(ms), 4), "glass_px": int(glass)}

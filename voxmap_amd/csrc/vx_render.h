@@ -1006,6 +1006,10 @@ __device__ __forceinline__ bool glass_scan(const KernelArgs &a, float d0, float 
         const float tb2 = d2 != 0.0f ? ((float)(c2 + (st2 > 0 ? e2 + 1 : -e2)) - o2) * iv2 : kInf;
         const int ax = (tb0 <= tb1 && tb0 <= tb2) ? 0 : (tb1 <= tb2 ? 1 : 2);
         const float te = ax == 0 ? tb0 : (ax == 1 ? tb1 : tb2);
+        // the walk's crossings never decrease, and a pane qualifies only nearer
+        // than tmax: past it no later entry can, so the scan ends there (each
+        // scan of the chain walks only up to the last surface written)
+        if (!(te < tmax)) break;
         auto side = [&](int c, float o, float d, int e) {
             const int v = f2i(floorf(o + te * d));
             const int lo = d < 0.0f ? c - e : c, hi = d < 0.0f ? c : c + e;
