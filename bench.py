@@ -45,7 +45,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-PMC_TAG = "r05"         # profiles/{traffic,valu}_<tag>[_c5].json: this round's rocprofv3 PMC summaries
+PMC_TAG = "r06"         # profiles/{traffic,valu}_<tag>[_c5].json: this round's rocprofv3 PMC summaries
 
 
 def parse(argv=None):
