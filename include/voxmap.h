@@ -30,7 +30,11 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 9
+/* ABI 10 (round 6): no signature or layout change; glass blends over the RGBA8
+ * canvas byte with clamped source and alpha (render.js:84-86, map.js:7), band /
+ * tile lists are cached per distinct list, no caller stream handle is kept,
+ * and a zeroed dist_cap falls back to VX_FALLBACK_DIST_CAP where 64 does not fit. */
+#define VX_ABI_VERSION 10
 
 /* error codes */
 #define VX_OK 0

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol(built):
     for n in names:
         assert hasattr(L, n), f"{n} missing from libvoxmap_hip.so"
     assert names == {s[0] for s in _abi.SIGNATURES}, names ^ {s[0] for s in _abi.SIGNATURES}
-    assert L.vx_abi_version() == _abi.ABI_VERSION == 9
+    assert L.vx_abi_version() == _abi.ABI_VERSION == 10
 
 
 def test_error_paths_do_not_touch_the_gpu(built):

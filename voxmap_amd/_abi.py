@@ -38,7 +38,8 @@ FLAG_REFLECT_ALL = 0x2000                       # ext: every first surface mirro
 FLAG_ROWS_BOTTOM_UP = 0x4000                    # diagnostics: blocks dispatched bottom row first (same frames)
 MAX_SHADOW_SAMPLES = 16
 DEFAULT_DIST_CAP = 64                           # vx_scene_desc.dist_cap = 0 (ABI 9; was 32)
-ABI_VERSION = 9
+FALLBACK_DIST_CAP = 32                          # dist_cap = 0 on a field the default cap does not fit (ABI 10)
+ABI_VERSION = 10
 PAL_SIZE, GLASS = 22, 21          # render.vert:21; air is B = PAL_SIZE in map.bin
 MGPU_UID_BYTES = 128
 
