@@ -134,6 +134,12 @@ extern "C" {
 /* Diagnostics (ABI 8): the frame's 32x8-pixel blocks dispatched bottom row first
  * (the launch's tail).  Identical frames. */
 #define VX_FLAG_ROWS_BOTTOM_UP 0x4000u
+/* Diagnostics: the frame's cone copy without the sun doom table (DESIGN.md §3
+ * "Doom table": cells from which every ray of the frame's sun window provably
+ * meets a solid cell within a few layers end the march unlit there).
+ * Identical frames; the shadow fetch counters count the steps the march takes
+ * without it.  VX_FLAG_SOFT_BRICK frames never use the doom table. */
+#define VX_FLAG_NO_DOOM 0x20000u
 #define VX_MAX_SHADOW_SAMPLES 16
 /* ABI 9: the default box cap of the primary traversal (vx_scene_desc.dist_cap
  * = 0).  64 since round 5 (was 32): fewer steps, 2x the octant copies' memory

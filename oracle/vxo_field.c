@@ -26,6 +26,7 @@
 #include "vxo.h"
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
@@ -277,4 +278,105 @@ void vxo_field_exit(const uint8_t *rgba, int X, int Y, int Z, int oct, int kx, i
         }
     }
     free(B); free(R); free(run);
+}
+
+/* ---------------- the sun doom table (DESIGN.md §3 "Doom table") ----------------
+ * In sun-aligned coordinates (x', y' grow toward the sun: x' = x if sx > 0,
+ * else X - 1 - x), a ray of the frame's samples rises one layer while x' grows
+ * by a slope in [ax_min, ax_max] (y' likewise).  Q = 4 sub-cells per cell and
+ * axis.  State S_z(g) (g a sub-cell (gx, gy) at height z, the bottom of layer
+ * z): every ray crossing height z inside g (within 1/64 cell) enters a solid
+ * cell (R = G = 0, sdf.cpp:430) before leaving the grid; depth(g) = layers to
+ * that entry.  Top-down:
+ *   depth_Z = inf (leaving the grid);
+ *   depth_z(g) = 0 if every cell covering g widened by 1/64 is solid,
+ *                else 1 + max over g' in g + [xlo, xhi] x [ylo, yhi] of depth_{z+1}(g')
+ * (sub-cells outside the grid: inf).  A cell (x', y', z) not solid is doomed
+ * with h = 1 + max over g' in [Q x' - 1, Q x' + Q + xhi] x [Q y' - 1, Q y' + Q
+ * + yhi] of depth_{z+1}(g'): from anywhere in the cell a ray meets height z + 1
+ * inside that window.  Depths saturate at 254 (inf = 255); h <= VXO_DOOM_HMAX. */
+void vxo_doom_plan(const float dirs[][3], int n, int *sx, int *sy, int *xlo, int *xhi, int *ylo, int *yhi) {
+    double axmin = 1e300, axmax = -1e300, aymin = 1e300, aymax = -1e300;
+    for (int k = 0; k < n; k++) {
+        const double ax = fabs((double)dirs[k][0] / (double)dirs[k][2]), ay = fabs((double)dirs[k][1] / (double)dirs[k][2]);
+        if (ax < axmin) axmin = ax;
+        if (ax > axmax) axmax = ax;
+        if (ay < aymin) aymin = ay;
+        if (ay > aymax) aymax = ay;
+    }
+    const double eps = 1.0 / 64.0, Q = (double)VXO_DOOM_Q;
+    *sx = dirs[0][0] > 0.0f ? 1 : -1;
+    *sy = dirs[0][1] > 0.0f ? 1 : -1;
+    *xlo = (int)floor(Q * (axmin - eps)); *xhi = (int)ceil(Q * (axmax + eps));
+    *ylo = (int)floor(Q * (aymin - eps)); *yhi = (int)ceil(Q * (aymax + eps));
+}
+
+void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, int sx, int sy, int xlo, int xhi, int ylo, int yhi,
+                    uint8_t *code) {
+    const int Q = VXO_DOOM_Q, GX = X * Q, GY = Y * Q;
+    const size_t XY = (size_t)X * Y, G = (size_t)GX * GY;
+    uint8_t *d1 = (uint8_t *)malloc(G), *d0 = (uint8_t *)malloc(G), *rx = (uint8_t *)malloc(G);
+    uint8_t *rc = (uint8_t *)malloc((size_t)GY * X);
+    memset(d1, 255, G);
+#define VXO_SOLID(z, xa, ya) ((xa) >= 0 && (xa) < X && (ya) >= 0 && (ya) < Y && \
+    rgba[4 * ((size_t)(z) * XY + (size_t)((sy > 0 ? (ya) : Y - 1 - (ya))) * X + (size_t)(sx > 0 ? (xa) : X - 1 - (xa)))] == 0 && \
+    rgba[4 * ((size_t)(z) * XY + (size_t)((sy > 0 ? (ya) : Y - 1 - (ya))) * X + (size_t)(sx > 0 ? (xa) : X - 1 - (xa))) + 1] == 0)
+    for (int z = Z - 1; z >= 0; z--) {
+        /* rows: rx(gy, gx) = max over [gx + xlo, gx + xhi], rc(gy, x') = max over [Q x' - 1, Q x' + Q + xhi] */
+#pragma omp parallel for schedule(static)
+        for (int gy = 0; gy < GY; gy++) {
+            const uint8_t *row = d1 + (size_t)gy * GX;
+            for (int gx = 0; gx < GX; gx++) {
+                int m = 0;
+                for (int k = gx + xlo; k <= gx + xhi; k++) {
+                    const int v = (k < 0 || k >= GX) ? 255 : row[k];
+                    if (v > m) m = v;
+                }
+                rx[(size_t)gy * GX + gx] = (uint8_t)m;
+            }
+            for (int x = 0; x < X; x++) {
+                int m = 0;
+                for (int k = Q * x - 1; k <= Q * x + Q + xhi; k++) {
+                    const int v = (k < 0 || k >= GX) ? 255 : row[k];
+                    if (v > m) m = v;
+                }
+                rc[(size_t)gy * X + x] = (uint8_t)m;
+            }
+        }
+        /* cells of layer z (from the states at z + 1) */
+#pragma omp parallel for schedule(static)
+        for (int y = 0; y < Y; y++) {
+            for (int x = 0; x < X; x++) {
+                int m = 0;
+                for (int k = Q * y - 1; k <= Q * y + Q + yhi; k++) {
+                    const int v = (k < 0 || k >= GY) ? 255 : rc[(size_t)k * X + x];
+                    if (v > m) m = v;
+                }
+                const int h = m + 1;
+                const int xr = sx > 0 ? x : X - 1 - x, yr = sy > 0 ? y : Y - 1 - y;
+                code[(size_t)z * XY + (size_t)yr * X + xr] =
+                    (uint8_t)((m < 255 && h <= VXO_DOOM_HMAX && !VXO_SOLID(z, x, y)) ? h + 1 : 0);
+            }
+        }
+        /* states at height z */
+#pragma omp parallel for schedule(static)
+        for (int gy = 0; gy < GY; gy++) {
+            const int y = gy / Q, b = gy % Q;
+            const int y0 = b == 0 ? y - 1 : y, y1 = b == Q - 1 ? y + 1 : y;    /* cells covering the sub-cell +- 1/64 */
+            for (int gx = 0; gx < GX; gx++) {
+                const int x = gx / Q, a = gx % Q;
+                const int x0 = a == 0 ? x - 1 : x, x1 = a == Q - 1 ? x + 1 : x;
+                const int es = VXO_SOLID(z, x0, y0) && VXO_SOLID(z, x1, y0) && VXO_SOLID(z, x0, y1) && VXO_SOLID(z, x1, y1);
+                int m = 0;
+                for (int l = gy + ylo; l <= gy + yhi; l++) {
+                    const int v = (l < 0 || l >= GY) ? 255 : rx[(size_t)l * GX + gx];
+                    if (v > m) m = v;
+                }
+                d0[(size_t)gy * GX + gx] = (uint8_t)(es ? 0 : (m < 255 ? (m + 1 < 254 ? m + 1 : 254) : 255));
+            }
+        }
+        uint8_t *t = d1; d1 = d0; d0 = t;
+    }
+#undef VXO_SOLID
+    free(d1); free(d0); free(rx); free(rc);
 }

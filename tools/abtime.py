@@ -5,7 +5,9 @@ own scene of the same grid, and renders the same frame into the same device
 framebuffer; rounds alternate between variants so clock/thermal drift hits
 all of them alike.  Reports the median ms per frame per variant and flags.
 
-usage: python tools/abtime.py [--config C3] [--flags 0,48] [--rounds 7] [--frames 20] label=path.so[:cap] ...
+usage: python tools/abtime.py [--config C3] [--flags 0,48] [--rounds 7] [--frames 20] label=path.so[:cap][+orflags] ...
+(+orflags: flags OR-ed into every frame of that variant, e.g. one library with
+and without a diagnostic flag, interleaved: head=lib.so nodoom=lib.so+131072)
 """
 from __future__ import annotations
 
@@ -43,6 +45,10 @@ def main():
     libs = []
     for spec in args.variants:
         label, path = spec.split("=", 1)
+        orf = 0
+        if "+" in path:                 # label=lib.so+FLAGS -- flags OR-ed into this variant's frames
+            path, orf = path.rsplit("+", 1)
+            orf = int(orf)
         cap = 0
         if ":" in path:                 # label=lib.so:CAP -- the scene's dist_cap (traversal box cap)
             path, cap = path.rsplit(":", 1)
@@ -65,18 +71,20 @@ def main():
         rc = L.vx_scene_create(C.byref(d), C.byref(h))
         if rc:
             raise SystemExit(f"{label}: {L.vx_last_error().decode()}")
-        libs.append((label, L, h))
+        libs.append((label, L, h, orf))
     out = torch.empty(W * H * 4, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     res = {}
     for flags in [int(f) for f in args.flags.split(",")]:
-        fr = presets.camera_frame(cfg["camera"], W, H, scale=up, flags=flags, shadow_samples=samples,
-                                  sun_radius=0.03 if samples > 1 else 0.0)
-        p = fr.params
-        times = {lab: [] for lab, _, _ in libs}
+        ps = {}
+        for lab, _, _, orf in libs:
+            ps[lab] = presets.camera_frame(cfg["camera"], W, H, scale=up, flags=flags | orf, shadow_samples=samples,
+                                           sun_radius=0.03 if samples > 1 else 0.0).params
+        times = {lab: [] for lab, _, _, _ in libs}
         for r in range(args.rounds + 1):
-            for lab, L, h in (libs if r % 2 == 0 else libs[::-1]):
+            for lab, L, h, _ in (libs if r % 2 == 0 else libs[::-1]):
+                p = ps[lab]
                 for _ in range(3):
                     L.vx_render(h, C.byref(p), W, H, _abi.PIXEL_RGBA8, C.c_void_p(out.data_ptr()), 1,
                                 C.c_void_p(stream.cuda_stream), None)
@@ -91,8 +99,8 @@ def main():
                 if r > 0:                       # round 0 warms everything up
                     times[lab].append(e0.elapsed_time(e1) / args.frames)
         ref = None                          # every variant's frame against the first one's
-        for lab, L, h in libs:
-            L.vx_render(h, C.byref(p), W, H, _abi.PIXEL_RGBA8, C.c_void_p(out.data_ptr()), 1,
+        for lab, L, h, _ in libs:
+            L.vx_render(h, C.byref(ps[lab]), W, H, _abi.PIXEL_RGBA8, C.c_void_p(out.data_ptr()), 1,
                         C.c_void_p(stream.cuda_stream), None)
             torch.cuda.synchronize()
             img = out.cpu()
@@ -102,13 +110,13 @@ def main():
                 print(f"{args.config} flags={flags:3d} {lab:14s} {int((img != ref).sum())} bytes differ from "
                       f"{libs[0][0]}", flush=True)
         base = None
-        for lab, _, _ in libs:
+        for lab, _, _, _ in libs:
             med = statistics.median(times[lab])
             base = base or med
             res[(lab, flags)] = med
             print(f"{args.config} flags={flags:3d} {lab:14s} median {med:.4f} ms  ({100 * (med / base - 1):+.1f}%)  "
                   f"min {min(times[lab]):.4f}", flush=True)
-    for lab, L, h in libs:
+    for lab, L, h, _ in libs:
         L.vx_scene_destroy(h)
 
 

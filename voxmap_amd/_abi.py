@@ -36,6 +36,7 @@ FLAG_GLASS_ORDER = 0x1000                       # diagnostics: the whole frame t
 FLAG_GLASS_SINGLE = 0x8000                      # diagnostics: nearest pane only (ABI <= 8); default = draw order
 FLAG_REFLECT_ALL = 0x2000                       # ext: every first surface mirrors the scene
 FLAG_ROWS_BOTTOM_UP = 0x4000                    # diagnostics: blocks dispatched bottom row first (same frames)
+FLAG_NO_DOOM = 0x20000                          # diagnostics: cone copy without the sun doom table (same frames)
 MAX_SHADOW_SAMPLES = 16
 DEFAULT_DIST_CAP = 64                           # vx_scene_desc.dist_cap = 0 (ABI 9; was 32)
 FALLBACK_DIST_CAP = 32                          # dist_cap = 0 on a field the default cap does not fit (ABI 10)

@@ -36,6 +36,8 @@ struct vx_scene {
     // (map.js:399-402), so one serves many frames
     struct Cone {
         int oct = -1, kx = -1, ky = -1;
+        bool doom = false;            // the doom table is in (launch_sun_doom, window `plan`)
+        int plan[6] = {0, 0, 0, 0, 0, 0};
         int8_t *d = nullptr;
         hipEvent_t ready = nullptr;   // recorded on the build's stream after the build
         unsigned long long used = 0;
@@ -430,12 +432,16 @@ struct TileSpec {
 // cache hit waits for the build's event until the host has seen it complete
 // (a no-op on the build's own stream).  t_build: recorded on st just before
 // the build's first packet (vx_prepare_sun's timing), if built.
-static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const int8_t **out, bool *built,
-                     vx_scene::Cone **used, hipEvent_t t_build) {
+// doom: the copy carries the doom table of window plan (DESIGN.md §3 "Doom
+// table"; part of the cache key).
+static int cone_copy(vx_scene *s, int oct, int kx, int ky, bool doom, const int plan[6], hipStream_t st,
+                     const int8_t **out, bool *built, vx_scene::Cone **used, hipEvent_t t_build) {
     *built = false;
     vx_scene::Cone *slot = nullptr;
     for (auto &c : s->cones)
-        if (c.d && c.oct == oct && c.kx == kx && c.ky == ky) slot = &c;
+        if (c.d && c.oct == oct && c.kx == kx && c.ky == ky && c.doom == doom &&
+            (!doom || std::memcmp(c.plan, plan, sizeof c.plan) == 0))
+            slot = &c;
     if (!slot) {
         slot = &s->cones[0];
         for (auto &c : s->cones)
@@ -450,11 +456,17 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
         slot->oct = -1;
         if (t_build) VX_HIP(hipEventRecord(t_build, st));
         VX_HIP(hipMemsetAsync(slot->d, 0xFF, (size_t)s->SXp * s->SYp * s->SZp, st));
-        const int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
+        int rc = launch_sun_cone(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, oct, kx, ky, st);
         if (rc) return set_error(VX_EDEVICE, std::string("sun cone copy: ") + hipGetErrorString((hipError_t)rc));
+        if (doom) {
+            rc = launch_sun_doom(s->d_sunp, slot->d, s->X, s->Y, s->Z, s->SB, plan, st);
+            if (rc) return set_error(VX_EDEVICE, std::string("sun doom table: ") + hipGetErrorString((hipError_t)rc));
+        }
         VX_HIP(hipEventRecord(slot->ready, st));
         slot->ready_seen = false;
         slot->oct = oct; slot->kx = kx; slot->ky = ky;
+        slot->doom = doom;
+        std::memcpy(slot->plan, plan, sizeof slot->plan);
         *built = true;
     } else if (!slot->ready_seen) {
         const hipError_t q = hipEventQuery(slot->ready);   // wait for the build
@@ -469,20 +481,27 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, hipStream_t st, const
 }
 
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
-// a.sunc (cone) built or found, and the info filled
+// a.sunc (cone) built or found, and the info filled.  A cone copy carries the
+// doom table unless the frame asks VX_FLAG_NO_DOOM or VX_FLAG_SOFT_BRICK (the
+// LDS brick march reads no doom codes); doom_k2 = 2 (kx + ky + 1) then, else 0.
 static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &fc, hipStream_t st,
                       const int8_t **sunc, vx_exit_info *info, bool *built, vx_scene::Cone **used,
-                      hipEvent_t t_build = nullptr) {
+                      int *doom_k2, hipEvent_t t_build = nullptr) {
     *sunc = nullptr;
     *used = nullptr;
+    if (doom_k2) *doom_k2 = 0;
     bool b = false;
     vx_exit_info e{0, -1, -1, -1, 0.0f};
     const bool tables = s->d_sunx && !(p->flags & VX_FLAG_NO_EXIT);
     if (tables && p->quality != 0 && !(p->flags & (VX_FLAG_NO_SHADOW | VX_FLAG_PRIMARY_ONLY))) {
         int oct, kx, ky;
         if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
-            const int rc = cone_copy(s, oct, kx, ky, st, sunc, &b, used, t_build);
+            const bool doom = !(p->flags & (VX_FLAG_NO_DOOM | VX_FLAG_SOFT_BRICK));
+            int plan[6] = {0, 0, 0, 0, 0, 0};
+            if (doom) doom_plan(fc, plan);
+            const int rc = cone_copy(s, oct, kx, ky, doom, plan, st, sunc, &b, used, t_build);
             if (rc) return rc;
+            if (doom && doom_k2) *doom_k2 = 2 * (kx + ky + 1);
             e = vx_exit_info{2, oct, kx, ky, 0.0f};
         } else if (fc.sun_k[0].fast) {
             const float *r = fc.sun_k[0].r;
@@ -544,7 +563,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     std::unique_lock<std::mutex> cone_lock(s->cone_mu);
     vx_scene::Cone *cone = nullptr;
     {
-        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
+        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone, &a.doom_k2);
         if (rc) return rc;
     }
     if (!cone) cone_lock.unlock();
@@ -623,7 +642,7 @@ int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_
         // ev0 is recorded inside cone_copy right before the build's first packet:
         // build_ms is the copy's GPU time, not the host's allocation or waits
         std::lock_guard<std::mutex> lock(s->cone_mu);
-        rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, s->ev0);
+        rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, nullptr, s->ev0);
         if (rc) return rc;
         if (built) VX_HIP(hipEventRecord(s->ev1, st));
     }

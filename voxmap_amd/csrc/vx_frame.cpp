@@ -180,4 +180,21 @@ int exit_plan(const FrameConsts &fc, int SB, int *oct, int *kx, int *ky) {
     *oct = sg0; *kx = cx; *ky = cy;
     return 1;
 }
+
+// vx_internal.h doom_plan; the oracle's vxo_doom_plan restated (same double
+// arithmetic on the same fp32 directions)
+void doom_plan(const FrameConsts &fc, int plan[6]) {
+    double axmin = 1e300, axmax = -1e300, aymin = 1e300, aymax = -1e300;
+    for (int k = 0; k < fc.n_sun; k++) {
+        const float *r = fc.sun_k[k].r;
+        const double ax = std::fabs((double)r[0] / (double)r[2]), ay = std::fabs((double)r[1] / (double)r[2]);
+        axmin = ax < axmin ? ax : axmin; axmax = ax > axmax ? ax : axmax;
+        aymin = ay < aymin ? ay : aymin; aymax = ay > aymax ? ay : aymax;
+    }
+    const double eps = 1.0 / 64.0, Q = (double)kDoomQ;
+    plan[0] = fc.sun_k[0].r[0] > 0.0f ? 1 : -1;
+    plan[1] = fc.sun_k[0].r[1] > 0.0f ? 1 : -1;
+    plan[2] = (int)std::floor(Q * (axmin - eps)); plan[3] = (int)std::ceil(Q * (axmax + eps));
+    plan[4] = (int)std::floor(Q * (aymin - eps)); plan[5] = (int)std::ceil(Q * (aymax + eps));
+}
 }  // namespace vx

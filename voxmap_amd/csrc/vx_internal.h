@@ -80,6 +80,7 @@ struct KernelArgs {
     unsigned SXpYp, sunp_texels;
     const int8_t *sunx;      // 8 orthant-exit copies of sunp's channel, one per ray octant (bit i: r_i > 0), or nullptr
     const int8_t *sunc;      // the frame's cone-exit copy (every sample of the frame reads it), or nullptr
+    int doom_k2;             // > 0: sunc carries doom codes (launch_sun_doom), 2 (kx + ky + 1) of its window
     const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *rg2;     // AO x-pairs (X + 1 per row): entry p = (R, G) of cells clamp(p - 1), clamp(p)
     const uint32_t *noise;   // RGBA8 noise texels
@@ -165,6 +166,16 @@ int launch_sun_exit(const int8_t *sunp, int8_t *sunx, uint8_t *flags, int X, int
 // |r_y/r_z| <= ky - 1/64 (layer recursion, kx, ky <= SB):
 int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, int oct, int kx, int ky,
                     void *stream);
+// The sun doom table (DESIGN.md §3 "Doom table", oracle vxo_field_doom): in a
+// cone copy already holding its exit marks and face bits, every cell from which
+// every ray of the sub-cell window {sx, sy, xlo, xhi, ylo, yhi} (doom_plan)
+// provably enters a solid cell h <= kDoomHMax layers up, and whose march texel
+// T is 1..kDoomTMax, becomes kDoomBase - (h * 8 + T - 1) (-11 .. -121).
+constexpr int kDoomQ = 4, kDoomHMax = 13, kDoomTMax = 8, kDoomBase = -10;
+int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[6], void *stream);
+// the doom table's window for a frame's samples (all fast, one octant, r_z > 0;
+// oracle vxo_doom_plan): sx, sy, then the per-layer sub-cell offsets xlo, xhi, ylo, yhi
+void doom_plan(const FrameConsts &fc, int plan[6]);
 // which copy a frame's sun march reads: 1 = one cone copy {oct, kx, ky} for every
 // sample (all on the fast path, one sign pattern, r_z > 0, slopes <= 4, kx, ky
 // <= SB); 0 = each fast sample its octant's orthant copy (oracle vxo_exit_plan)

@@ -492,6 +492,84 @@ __global__ void k_sun_cone_layer(const int8_t *ch, int8_t *out, int X, int Y, in
         }
     out[p] = d ? (int8_t)-1 : ch[p];
 }
+// ---- one layer z of the sun doom table (oracle vxo_field_doom; DESIGN.md §3
+// "Doom table"), sun-aligned coordinates (x' = x if sx > 0, else X - 1 - x).
+// d1 = the sub-cell states at height z + 1 (GX x GY, 255 = leaves the grid),
+// d0 = those at height z.  A block takes 8 x 8 cells = 32 x 32 sub-cells: it
+// stages d1 over the sub-cells its windows reach (the cells' [4 x' - 1, 4 x' +
+// 4 + xhi] and the states' [gx + xlo, gx + xhi], xlo >= -1), takes the window
+// maxima separably in LDS (rows, then columns), writes d0 and turns each
+// doomed cell of the cone copy whose march texel T is 1..kDoomTMax into its
+// code.  Solid = R = G = 0 (sdf.cpp:430) inside the grid.
+constexpr int kDoomT = 8, kDoomS = kDoomT * kDoomQ, kDoomW = kDoomS + 2 + 17 + 1;   // xhi <= 17 (|r_x / r_z| <= 4)
+__global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t np, int8_t *sunc, const uint8_t *d1,
+                                                    uint8_t *d0, int X, int Y, int z, int SB, int SXp, size_t SXpYp,
+                                                    int sx, int sy, int xlo, int xhi, int ylo, int yhi) {
+    __shared__ uint8_t s_d[kDoomW][kDoomW];       // d1 rows H0 - 1 .., columns G0 - 1 ..
+    __shared__ uint8_t s_rx[kDoomW][kDoomS];      // row maxima over the states' x windows
+    __shared__ uint8_t s_rc[kDoomW][kDoomT];      // row maxima over the cells' x windows
+    __shared__ uint8_t s_solid[kDoomT + 2][kDoomT + 2];
+    const int GX = X * kDoomQ, GY = Y * kDoomQ;
+    const int x0 = blockIdx.x * kDoomT, y0 = blockIdx.y * kDoomT;          // aligned cells
+    const int G0 = x0 * kDoomQ, H0 = y0 * kDoomQ;
+    const int W = kDoomS + 2 + xhi, H = kDoomS + 2 + yhi;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < W * H; k += 256) {
+        const int r = k / W, c = k - r * W;
+        const int gx = G0 - 1 + c, gy = H0 - 1 + r;
+        s_d[r][c] = (gx < 0 || gx >= GX || gy < 0 || gy >= GY) ? (uint8_t)255 : d1[(size_t)gy * GX + gx];
+    }
+    auto real = [&](int xa, int ya) {            // padded offset of aligned cell (xa, ya, z)
+        const int xr = sx > 0 ? xa : X - 1 - xa, yr = sy > 0 ? ya : Y - 1 - ya;
+        return (size_t)(xr + SB) + (size_t)SXp * (size_t)(yr + SB) + SXpYp * (size_t)(z + SB);
+    };
+    if (tid < (kDoomT + 2) * (kDoomT + 2)) {
+        const int j = tid / (kDoomT + 2), i = tid - j * (kDoomT + 2);
+        const int xa = x0 - 1 + i, ya = y0 - 1 + j;
+        bool solid = false;
+        if (xa >= 0 && xa < X && ya >= 0 && ya < Y) {
+            const size_t p = real(xa, ya);
+            solid = sunp[p] == 0 && sunp[np + p] == 0;
+        }
+        s_solid[j][i] = solid ? 1 : 0;
+    }
+    __syncthreads();
+    for (int k = tid; k < H * (kDoomS + kDoomT); k += 256) {
+        const int r = k / (kDoomS + kDoomT), c = k - r * (kDoomS + kDoomT);
+        int lo, hi;
+        if (c < kDoomS) { lo = c + 1 + xlo; hi = c + 1 + xhi; }            // sub-cell G0 + c
+        else { lo = kDoomQ * (c - kDoomS); hi = lo + kDoomQ + 1 + xhi; }    // cell x0 + (c - kDoomS)
+        int m = 0;
+        for (int q = lo; q <= hi; q++) m = max(m, (int)s_d[r][q]);
+        if (c < kDoomS) s_rx[r][c] = (uint8_t)m; else s_rc[r][c - kDoomS] = (uint8_t)m;
+    }
+    __syncthreads();
+    for (int k = tid; k < kDoomS * kDoomS; k += 256) {                     // states at height z
+        const int j = k / kDoomS, i = k - j * kDoomS;
+        const int gx = G0 + i, gy = H0 + j;
+        if (gx >= GX || gy >= GY) continue;
+        int m = 0;
+        for (int r = j + 1 + ylo; r <= j + 1 + yhi; r++) m = max(m, (int)s_rx[r][i]);
+        const int ci = i / kDoomQ, a = i % kDoomQ, cj = j / kDoomQ, b = j % kDoomQ;
+        const int xa0 = ci + 1 - (a == 0 ? 1 : 0), xa1 = ci + 1 + (a == kDoomQ - 1 ? 1 : 0);   // in s_solid
+        const int ya0 = cj + 1 - (b == 0 ? 1 : 0), ya1 = cj + 1 + (b == kDoomQ - 1 ? 1 : 0);
+        const bool es = s_solid[ya0][xa0] && s_solid[ya0][xa1] && s_solid[ya1][xa0] && s_solid[ya1][xa1];
+        d0[(size_t)gy * GX + gx] = (uint8_t)(es ? 0 : (m < 255 ? min(m + 1, 254) : 255));
+    }
+    if (tid < kDoomT * kDoomT) {                                            // cells of layer z
+        const int j = tid / kDoomT, i = tid - j * kDoomT;
+        const int xa = x0 + i, ya = y0 + j;
+        if (xa < X && ya < Y && !s_solid[j + 1][i + 1]) {
+            int m = 0;
+            for (int r = kDoomQ * j; r <= kDoomQ * j + kDoomQ + 1 + yhi; r++) m = max(m, (int)s_rc[r][i]);
+            if (m < 255 && m + 1 <= kDoomHMax) {
+                const size_t p = real(xa, ya);
+                const int t = sunc[p];
+                if (t >= 1 && t <= kDoomTMax) sunc[p] = (int8_t)(kDoomBase - (m * 8 + t - 1));
+            }
+        }
+    }
+}
 // map.bin B -> the traversal's vis colour, in place in the linear upload (B
 // kept in bcol for vx_scene_read_field): the meshed palette indices 1..21
 // (sdf.cpp:284 meshes colours < pal_size = 22; render.vert:21) stay, anything
@@ -651,6 +729,31 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
     hipLaunchKernelGGL(k_exit_face_bits, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, sunc, X, Y, Z, SB, SXp,
                        SXpYp, sx, sy, 1);
     return (int)hipGetLastError();
+}
+
+int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[6], void *stream) {
+    const int sx = plan[0], sy = plan[1], xlo = plan[2], xhi = plan[3], ylo = plan[4], yhi = plan[5];
+    // the block's staged window (k_doom_layer): xlo, ylo >= -1, xhi, yhi <= 17
+    if (xlo < -1 || ylo < -1 || xhi > 17 || yhi > 17 || xlo > xhi || ylo > yhi || SB < 1)
+        return (int)hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    const int SXp = X + 2 * SB, SYp = Y + 2 * SB, SZp = Z + 2 * SB;
+    const size_t SXpYp = (size_t)SXp * SYp, np = SXpYp * SZp;
+    const size_t G = (size_t)X * Y * kDoomQ * kDoomQ;
+    uint8_t *d[2] = {nullptr, nullptr};
+    hipError_t e = hipMallocAsync((void **)&d[0], 2 * G, s);
+    if (e != hipSuccess) return (int)e;
+    d[1] = d[0] + G;
+    e = hipMemsetAsync(d[0], 0xFF, G, s);                 // above the top layer: leaves the grid
+    if (e == hipSuccess) {
+        const dim3 grid((unsigned)((X + kDoomT - 1) / kDoomT), (unsigned)((Y + kDoomT - 1) / kDoomT));
+        for (int z = Z - 1, k = 0; z >= 0; z--, k ^= 1)
+            hipLaunchKernelGGL(k_doom_layer, grid, dim3(256), 0, s, sunp, np, sunc, d[k], d[k ^ 1], X, Y, z, SB, SXp,
+                               SXpYp, sx, sy, xlo, xhi, ylo, yhi);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(d[0], s);
+    return (int)(e != hipSuccess ? e : f);
 }
 
 int launch_field_unpack(const uint16_t *rg, const uint8_t *bcol, const uint32_t *prim_copy, uint32_t *out, int X,

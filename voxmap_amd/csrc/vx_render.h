@@ -440,7 +440,7 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
         exy += __builtin_fmaf(fl1, xpf, fl0); e2 += fl2;                          // :119 (exact)
         return __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy);
     };
-    int step = 0;                                                                // wave-uniform
+    int step = 0;                              // landings taken
     const unsigned nl = active_lanes();
     if (maxs > 1) {                            // the first step, peeled: its len from march_len_sg
         const float t = ld_fmt1(rsrc, advance());                                  // :123-128
@@ -449,17 +449,32 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
         tv = t;
         cnt.march_witers += once_per_wave(1u);
         cnt.march_slots += once_per_wave(nl);
-        ++step;
+        step = 1;
     }
-    if (maxs > 1 && tv > 0.0f && step < maxs - 1) {
-        do {
-            const float t = ld_fmt1(rsrc, advance());
-            len = march_len_fract<SG>(S, f0, f1, f2);   // next step, under the load
-            cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
-            tv = t;
-            cnt.march_witers += once_per_wave(1u);   // counted in the loop: step stays a scalar
-            cnt.march_slots += once_per_wave(nl);
-        } while (tv > 0.0f && ++step < maxs - 1);
+    auto run = [&]() {                         // steps until a non-positive texel or landing MAX_STEPS-1
+        if (tv > 0.0f && step < maxs - 1) {
+            do {
+                const float t = ld_fmt1(rsrc, advance());
+                len = march_len_fract<SG>(S, f0, f1, f2);   // next step, under the load
+                cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
+                tv = t;
+                cnt.march_witers += once_per_wave(1u);
+                cnt.march_slots += once_per_wave(nl);
+            } while (tv > 0.0f && ++step < maxs - 1);
+            step += tv > 0.0f ? 0 : 1;
+        }
+    };
+    if (maxs > 1) run();
+    // A doom code (only a doom frame's cone copy holds them, launch_sun_doom):
+    // landing `step` is in a cell from which every ray of the frame's window
+    // meets a solid cell h layers up, so the march lands on a 0 texel within
+    // (h + 1) 2 (kx + ky + 1) landings -- unlit, if that is before MAX_STEPS
+    // (oracle march_ex); else the march goes on from the cell's texel T.
+    while (tv <= -9.5f) {
+        const int u = (int)(-10.0f - tv);
+        if (step + ((u >> 3) + 2) * a.doom_k2 < maxs) { tv = 0.0f; break; }
+        tv = (float)((u & 7) + 1);
+        run();
     }
     if (tv > 0.0f) {                           // the MAX_STEPS-th step: only its fetch (stats) matters
         const float t = ld_fmt1(rsrc, advance());   // (dropped unless counted)
@@ -636,7 +651,7 @@ __device__ __forceinline__ bool first_step_exit(const KernelArgs &a, const int8_
     // the air cell is inside the padded copy (a face lies inside the grid or on its edge)
     const unsigned off = (unsigned)(x + a.SB) + (unsigned)a.SXp * (unsigned)(y + a.SB) + a.SXpYp * (unsigned)(z + a.SB);
     const float v = ok ? ld_fmt1(buf_rsrc(ch, kRsrcS8), off) : 0.0f;
-    return v <= -2.0f && (((int)(-1.0f - v) >> ax) & 1);
+    return v <= -2.0f && v >= -8.5f && (((int)(-1.0f - v) >> ax) & 1);   // face bits, not a doom code
 }
 
 // march(cell, fract, S.r) of render.frag:233 -> "lit" (step == MAX_STEPS, :234).
