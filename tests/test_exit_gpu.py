@@ -247,6 +247,7 @@ def _literal_subset(sc, fr, W, H, O, every=16):
     assert fr.params.flags & vx.FLAG_NO_EXIT
     ids = list(range(0, -(-H // 8), every))
     out = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()            # the fill (torch's stream) before the scene's stream writes
     st = sc.render_bands(fr, 8, ids, out.data_ptr(), inplace=True, pixel_format=vx.PIXEL_RGBA32F, stats=True)
     torch.cuda.synchronize()
     img = out.cpu().numpy()

@@ -82,6 +82,7 @@ def test_two_threads_render_different_band_lists(scene):
         try:
             st = torch.cuda.Stream()
             buf = torch.zeros(H * W * 4, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()     # the fill on torch's stream before st uses the buffer
             for rep in range(16):
                 ids = lists[tid][rep % 2]
                 with torch.cuda.stream(st):
@@ -127,6 +128,7 @@ def test_tile_lists_from_two_threads(scene):
             st = torch.cuda.Stream()
             tiles = torch.empty(n * TS * TS * 4, dtype=torch.uint8, device="cuda")
             frame = torch.zeros(H * W * 4, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()     # the fill on torch's stream before st uses the buffer
             for rep in range(12):
                 ids = lists[tid][rep % 2]
                 with torch.cuda.stream(st):

@@ -196,6 +196,7 @@ def test_tiles_and_detile_equal_full_frame(full_scene, flags, samples):
     ids = list(range(tx * ty))[::-1]    # any order
     tiles = torch.empty(len(ids) * ts * ts * 4, dtype=torch.uint8, device="cuda:0")
     frame = torch.zeros(h * w * 4, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()            # the fill (torch's stream) before the scene's stream writes
     sc.render_tiles(fr, ts, ids, tiles.data_ptr())
     sc.detile(w, h, ts, ids, tiles.data_ptr(), frame.data_ptr())
     torch.cuda.synchronize()
@@ -424,7 +425,9 @@ def test_soft_pool_equals_per_sample_march(noise):
     """VX_FLAG_SOFT_POOL and VX_FLAG_SOFT_BRICK at C5 (3^3 field, 16 samples,
     full quality): the pooled wave march, with and without LDS brick staging,
     gives the same RGBA8 frame and the same work counters as the per-sample
-    loop, on the whole 3840x2160 frame."""
+    loop, on the whole 3840x2160 frame.  The brick march reads no doom table
+    (DESIGN.md §3 "Doom table"): its counters are the per-sample loop's with
+    VX_FLAG_NO_DOOM."""
     import torch
     import voxmap_amd as vx
     from voxmap_amd import presets
@@ -434,16 +437,18 @@ def test_soft_pool_equals_per_sample_march(noise):
     outs, sts = [], []
     with vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_bytes=noise.tobytes(),
                   noise_format=vx.FORMAT_BIN, dims=(X, Y, Z), device=0) as sc:
-        for extra in (0, vx.FLAG_SOFT_POOL, vx.FLAG_SOFT_BRICK):
+        for extra in (0, vx.FLAG_SOFT_POOL, vx.FLAG_SOFT_BRICK, vx.FLAG_NO_DOOM):
             fr = presets.camera_frame("K1", c["w"], c["h"], scale=3.0, flags=vx.FLAG_FULL_QUALITY | extra,
                                       shadow_samples=16, sun_radius=0.03)
             out = torch.zeros(c["w"] * c["h"] * 4, dtype=torch.uint8, device="cuda:0")
+            torch.cuda.synchronize()         # the fill (torch's stream) before the scene's stream writes
             sts.append(sc.render_device(fr, out.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True))
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy())
-    for i in (1, 2):
+    for i in (1, 2, 3):
         assert np.array_equal(outs[0], outs[i]), i
-        a, b = sts[0].as_dict(), sts[i].as_dict()
+    for i, j in ((0, 1), (3, 2)):
+        a, b = sts[i].as_dict(), sts[j].as_dict()
         for k in ("shadow_rays", "shadow_fetches", "primary_fetches", "ao_samples", "alg_bytes"):
             assert a[k] == b[k], (i, k, a[k], b[k])
 
@@ -512,6 +517,7 @@ def test_bands_inplace_and_compact_equal_full_frame(full_scene, fmt):
     full, _ = sc.render(fr, pixel_format=pf)
     nb = -(-h // br)
     frame = torch.full((h, w, ch), 7, dtype=dt, device="cuda:0")
+    torch.cuda.synchronize()                 # the fill (torch's stream) before the scene's stream writes
     for world in (3,):
         for r in range(world):                        # every rank's deal, in place in one frame
             sc.render_bands(fr, br, vx.mgpu_bands(h, br, world, r), frame.data_ptr(), inplace=True, pixel_format=pf)
@@ -520,6 +526,7 @@ def test_bands_inplace_and_compact_equal_full_frame(full_scene, fmt):
     assert np.array_equal(got.view(np.uint8), full.view(np.uint8))
     ids = list(range(nb))[::-1]                       # compact, any order
     comp = torch.zeros((nb * br, w, ch), dtype=dt, device="cuda:0")
+    torch.cuda.synchronize()
     sc.render_bands(fr, br, ids, comp.data_ptr(), inplace=False, pixel_format=pf)
     torch.cuda.synchronize()
     comp = comp.cpu().numpy()
@@ -541,6 +548,7 @@ def test_mgpu_single_rank_equals_full_frame(full_scene):
     mg = vx.MultiGPU(sc, vx.mgpu_unique_id(), 1, 0)
     try:
         frame = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()                     # the fill before the scene's stream writes
         st = mg.render(fr, 64, frame.data_ptr(), stats=True)
         mg.gather(w, h, 64, frame.data_ptr())        # the gather step alone (bench's split timing)
         torch.cuda.synchronize()
@@ -584,6 +592,7 @@ def test_c4_full_frame_as_eight_rank_band_lists(full_scene, noise):
     w, h, br = c["w"], c["h"], 64
     fr = presets.camera_frame(c["camera"], w, h, flags=vx.FLAG_FULL_QUALITY)
     frame = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()                 # the fill (torch's stream) before the scene's stream writes
     for r in range(8):
         sc.render_bands(fr, br, vx.mgpu_bands(h, br, 8, r), frame.data_ptr(), inplace=True,
                         pixel_format=vx.PIXEL_RGBA32F)
@@ -596,6 +605,7 @@ def test_c4_full_frame_as_eight_rank_band_lists(full_scene, noise):
     whole = torch.empty((h, w, 4), dtype=torch.uint8, device="cuda:0")
     sc.render_device(fr, whole.data_ptr(), pixel_format=vx.PIXEL_RGBA8)
     f8 = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
     for r in range(8):
         sc.render_bands(fr, br, vx.mgpu_bands(h, br, 8, r), f8.data_ptr(), inplace=True)
     torch.cuda.synchronize()

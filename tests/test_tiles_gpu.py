@@ -45,6 +45,7 @@ def test_more_than_65535_tiles_take_the_1d_grid(scene, flags):
     w, h, ts = 8224, 8192, 32
     fr = presets.camera_frame("K1", w, h, flags=flags)
     full = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()            # the fill (torch's stream) before the scene's stream writes
     scene.render_device(fr, full.data_ptr(), pixel_format=vx.PIXEL_RGBA8)
     n = (w // ts) * (h // ts)
     assert n > 65535
@@ -52,6 +53,7 @@ def test_more_than_65535_tiles_take_the_1d_grid(scene, flags):
     tiles = torch.empty(n * ts * ts * 4, dtype=torch.uint8, device="cuda:0")
     scene.render_tiles(fr, ts, ids, tiles.data_ptr())
     frame = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
     scene.detile(w, h, ts, ids, tiles.data_ptr(), frame.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(frame, full)
@@ -75,6 +77,7 @@ def test_single_block_row_bands_and_compact_bands(scene, inplace):
     ids = list(range(0, h // 8, 3))
     for one in (ids, ids[:1]):
         out = torch.zeros((h if inplace else len(one) * 8) * w * 4, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()        # the fill (torch's stream) before the scene's stream writes
         scene.render_bands(fr, 8, one, out.data_ptr(), inplace=bool(inplace), pixel_format=vx.PIXEL_RGBA8)
         torch.cuda.synchronize()
         img = out.cpu().numpy().reshape(-1, w, 4)

@@ -24,7 +24,7 @@ def main():
         sc = vx.Scene(map_bytes=grid.tobytes(), map_format=vx.FORMAT_GRID, noise_path=scenes.NOISE_PATH,
                       dims=(X, Y, Z), device=0)
         scale = 3.0 if c["scene"] == "s_up3" else 1.0
-        n = c.get("samples", 0)
+        n = 16                            # soft shadows: the frames that read the doom table
         r = {}
         for name, fl in (("no_doom", vx.FLAG_NO_DOOM), ("doom", 0), ("no_doom_again", vx.FLAG_NO_DOOM),
                          ("doom_again", 0)):

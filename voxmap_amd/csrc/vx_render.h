@@ -421,7 +421,25 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
 // offset terms, len = the first step's length (march_len_sg), rsrc = the
 // channel's typed-load descriptor (march_pad; march_soft shares these across
 // the samples of a fragment).
-template <int SG>
+// A doom code (soft-shadow frames' cone copies, launch_sun_doom) read at
+// landing j: the cell is one from which every ray of the frame's window meets
+// a solid cell h layers up, so the march lands on a 0 texel within (h + 1) 2
+// (kx + ky + 1) landings -- unlit (0) if that is before MAX_STEPS, else the
+// march goes on from the cell's texel T (oracle march_ex).  Anything else is
+// returned as read.
+__device__ __forceinline__ float doom_resolve(const KernelArgs &a, float t, int j, int maxs) {
+    if (t <= -9.5f) {
+        const int u = (int)(-10.0f - t);
+        t = j + ((u >> 3) + 2) * a.doom_k2 < maxs ? 0.0f : (float)((u & 7) + 1);
+    }
+    return t;
+}
+
+// DOOM: the copy may hold doom codes.  The peeled first landing resolves its
+// own; a code read in the loop ends the loop like any negative value and is
+// resolved after it (landing step + 1), a late one marching on in a per-lane
+// loop of its own, so the main loop keeps its scalar step count.
+template <int SG, bool DOOM = false>
 __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay &S, u32x4 rsrc, float exy, float e2,
                                                float len, float f0, float f1, float f2, Counters &cnt) {
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
@@ -440,41 +458,42 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
         exy += __builtin_fmaf(fl1, xpf, fl0); e2 += fl2;                          // :119 (exact)
         return __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy);
     };
-    int step = 0;                              // landings taken
+    int step = 0;                                                                // wave-uniform
     const unsigned nl = active_lanes();
     if (maxs > 1) {                            // the first step, peeled: its len from march_len_sg
-        const float t = ld_fmt1(rsrc, advance());                                  // :123-128
+        float t = ld_fmt1(rsrc, advance());                                        // :123-128
         len = march_len_sg<SG>(S, f0, f1, f2);  // next step, under the load
         cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
+        if constexpr (DOOM) t = doom_resolve(a, t, 1, maxs);
         tv = t;
         cnt.march_witers += once_per_wave(1u);
         cnt.march_slots += once_per_wave(nl);
-        step = 1;
+        ++step;
     }
-    auto run = [&]() {                         // steps until a non-positive texel or landing MAX_STEPS-1
-        if (tv > 0.0f && step < maxs - 1) {
-            do {
-                const float t = ld_fmt1(rsrc, advance());
-                len = march_len_fract<SG>(S, f0, f1, f2);   // next step, under the load
-                cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
-                tv = t;
-                cnt.march_witers += once_per_wave(1u);
-                cnt.march_slots += once_per_wave(nl);
-            } while (tv > 0.0f && ++step < maxs - 1);
-            step += tv > 0.0f ? 0 : 1;
+    if (maxs > 1 && tv > 0.0f && step < maxs - 1) {
+        int j = 1;                             // DOOM: the lane's landings (the loop's exit leaves step behind)
+        do {
+            float t = ld_fmt1(rsrc, advance());
+            len = march_len_fract<SG>(S, f0, f1, f2);   // next step, under the load
+            cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
+            tv = t;
+            if constexpr (DOOM) ++j;
+            cnt.march_witers += once_per_wave(1u);   // counted in the loop: step stays a scalar
+            cnt.march_slots += once_per_wave(nl);
+        } while (tv > 0.0f && ++step < maxs - 1);
+        if constexpr (DOOM) {
+            if (tv <= -9.5f) {                 // a doom code at landing j
+                tv = doom_resolve(a, tv, j, maxs);
+                while (tv > 0.0f && j < maxs - 1) {   // late: on from the cell's texel (rare)
+                    float t2 = ld_fmt1(rsrc, advance());
+                    len = march_len_fract<SG>(S, f0, f1, f2);
+                    cnt.shadow_fetch += t2 >= 0.0f ? 1u : 0u;
+                    cnt.march_witers += once_per_wave(1u);
+                    cnt.march_slots += once_per_wave(nl);
+                    tv = doom_resolve(a, t2, ++j, maxs);
+                }
+            }
         }
-    };
-    if (maxs > 1) run();
-    // A doom code (only a doom frame's cone copy holds them, launch_sun_doom):
-    // landing `step` is in a cell from which every ray of the frame's window
-    // meets a solid cell h layers up, so the march lands on a 0 texel within
-    // (h + 1) 2 (kx + ky + 1) landings -- unlit, if that is before MAX_STEPS
-    // (oracle march_ex); else the march goes on from the cell's texel T.
-    while (tv <= -9.5f) {
-        const int u = (int)(-10.0f - tv);
-        if (step + ((u >> 3) + 2) * a.doom_k2 < maxs) { tv = 0.0f; break; }
-        tv = (float)((u & 7) + 1);
-        run();
     }
     if (tv > 0.0f) {                           // the MAX_STEPS-th step: only its fetch (stats) matters
         const float t = ld_fmt1(rsrc, advance());   // (dropped unless counted)
@@ -483,7 +502,7 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
     return tv != 0.0f;
 }
 
-template <int SG>   // the sun's axis signs (bit i: r_i > 0)
+template <int SG, bool DOOM = false>   // the sun's axis signs (bit i: r_i > 0); DOOM: see march_pad_from
 __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, float c0, float c1,
                                           float c2, float f0, float f1, float f2, Counters &cnt) {
     const float xpf = (float)a.SXp;
@@ -491,7 +510,7 @@ __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, 
     const float exy = __builtin_fmaf(c1 + a.SBf, xpf, (c0 + a.SBf) + kBias);   // exact integers
     const float e2 = (c2 + a.SBf) + kBias;
     const u32x4 rsrc = buf_rsrc(sun - 0x4B000000, kRsrcS8);   // (pointer arithmetic: keeps the global address space)
-    return march_pad_from<SG>(a, S, rsrc, exy, e2, march_len_sg<SG>(S, f0, f1, f2), f0, f1, f2, cnt);
+    return march_pad_from<SG, DOOM>(a, S, rsrc, exy, e2, march_len_sg<SG>(S, f0, f1, f2), f0, f1, f2, cnt);
 }
 
 // The soft-shadow samples of one fragment (every sample on the padded path with
@@ -514,7 +533,7 @@ __device__ __forceinline__ int march_soft(const KernelArgs &a, const int8_t *sun
     for (int k = 0; k < F.n_sun; k++) {
         cnt.shadow_rays++;
         const SunRay S = F.sun_k[k];
-        lit += march_pad_from<SG>(a, S, rsrc, exy, e2, march_len_d(S, d0, d1, d2), f0, f1, f2, cnt) ? 1 : 0;
+        lit += march_pad_from<SG, true>(a, S, rsrc, exy, e2, march_len_d(S, d0, d1, d2), f0, f1, f2, cnt) ? 1 : 0;
     }
     return lit;
 }
@@ -1875,11 +1894,11 @@ void k_render(KernelArgs a) {
                             }
                         } else {
                             switch (sgv) {
-#define VX_SGP(K) case K: lit = march_pad<K>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
-                                             cnt); break;
+#define VX_SGP(K) case K: lit = march_pad<K, true>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
+                                                   cnt); break;
                                 VX_SGP(0) VX_SGP(1) VX_SGP(2) VX_SGP(3) VX_SGP(4) VX_SGP(5) VX_SGP(6)
-                                default: lit = march_pad<7>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
-                                                            cnt);
+                                default: lit = march_pad<7, true>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
+                                                                  cnt);
 #undef VX_SGP
                             }
                         }
