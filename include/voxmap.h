@@ -33,7 +33,8 @@ extern "C" {
 /* ABI 10 (round 6): no signature or layout change; glass blends over the RGBA8
  * canvas byte with clamped source and alpha (render.js:84-86, map.js:7), band /
  * tile lists are cached per distinct list, no caller stream handle is kept,
- * and a zeroed dist_cap falls back to VX_FALLBACK_DIST_CAP where 64 does not fit. */
+ * a zeroed dist_cap falls back to VX_FALLBACK_DIST_CAP where 64 does not fit,
+ * and soft-shadow frames read the sun doom table (VX_FLAG_NO_DOOM: without). */
 #define VX_ABI_VERSION 10
 
 /* error codes */

@@ -25,7 +25,7 @@ class OScene(C.Structure):
                 ("noise_w", C.c_int), ("noise_h", C.c_int), ("oct_e", C.c_void_p * 8), ("fp2d", C.c_void_p),
                 ("exit_mode", C.c_int), ("held", C.c_void_p), ("held_oct", C.c_int), ("held_kx", C.c_int),
                 ("held_ky", C.c_int), ("qoff", C.c_void_p), ("chunk", C.c_int), ("unit_split", C.c_int),
-                ("held_doom", C.c_void_p), ("held_dplan", C.c_int * 6)]
+                ("held_doom", C.c_void_p), ("held_dplan", C.c_int * 7)]
 
 
 class OStats(C.Structure):
@@ -89,9 +89,9 @@ def lib():
         L.vxo_exit_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_int)]
         L.vxo_exit_plan.restype = C.c_int
-        L.vxo_doom_plan.argtypes = [C.c_void_p, C.c_int] + [C.POINTER(C.c_int)] * 6
+        L.vxo_doom_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
         L.vxo_doom_plan.restype = None
-        L.vxo_field_doom.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int] + [C.c_int] * 6 + [C.c_void_p]
+        L.vxo_field_doom.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_void_p]
         L.vxo_field_doom.restype = None
         L.vxo_face_quads.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.vxo_face_quads.restype = None
@@ -166,10 +166,12 @@ class Oracle:
         self.sc.held = self._held.ctypes.data
         self.sc.held_oct, self.sc.held_kx, self.sc.held_ky = octs[0], kx, ky
         if cone and len(d) > 1 and not (params.flags & (0x20000 | 0x100)):   # soft shadows: the doom table
-            plan = doom_plan(d)
-            self._held_doom = field_doom(self.field, *plan)
-            self.sc.held_doom = self._held_doom.ctypes.data
-            self.sc.held_dplan = (C.c_int * 6)(*plan)
+            Z = self.sc.Z
+            plan = doom_plan(d, params.max_shadow_steps if params.max_shadow_steps > 0 else 2 * Z, kx, ky)
+            if plan[6] >= 1:
+                self._held_doom = field_doom(self.field, plan)
+                self.sc.held_doom = self._held_doom.ctypes.data
+                self.sc.held_dplan = (C.c_int * 7)(*plan)
         return octs[0], kx, ky
 
     def render(self, params, w: int, h: int, row0: int = 0, row_step: int = 1, threads: int = 0, out=None):
@@ -303,22 +305,24 @@ def field_exit(field_zyx4: np.ndarray, oct: int, kx: int = -1, ky: int = -1) -> 
     return out
 
 
-def doom_plan(dirs):
-    """(sx, sy, xlo, xhi, ylo, yhi): the doom table's sub-cell window for a
-    frame's sun samples (vxo_doom_plan; all fast, one octant, r_z > 0)."""
+def doom_plan(dirs, max_steps: int, kx: int, ky: int):
+    """(sx, sy, xlo, xhi, ylo, yhi, hmax): the doom table's sub-cell window for
+    a frame's sun samples (vxo_doom_plan; all fast, one octant, r_z > 0) and the
+    largest h its stop rule can use at MAX = max_steps with cone window kx, ky."""
     d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
-    v = [C.c_int() for _ in range(6)]
-    lib().vxo_doom_plan(d.ctypes.data, d.shape[0], *[C.byref(x) for x in v])
-    return tuple(x.value for x in v)
+    v = (C.c_int * 7)()
+    lib().vxo_doom_plan(d.ctypes.data, d.shape[0], int(max_steps), int(kx), int(ky), v)
+    return tuple(v)
 
 
-def field_doom(field_zyx4: np.ndarray, sx: int, sy: int, xlo: int, xhi: int, ylo: int, yhi: int) -> np.ndarray:
+def field_doom(field_zyx4: np.ndarray, plan) -> np.ndarray:
     """(Z, Y, X) uint8: the sun doom table (vxo_field_doom): h + 1
-    where every ray of the window provably enters a solid cell h layers up, else 0."""
+    where every ray of the window provably enters a solid cell h <= hmax layers
+    up, else 0."""
     f = np.ascontiguousarray(field_zyx4, np.uint8)
     Z, Y, X, _ = f.shape
     out = np.empty((Z, Y, X), np.uint8)
-    lib().vxo_field_doom(f.ctypes.data, X, Y, Z, sx, sy, xlo, xhi, ylo, yhi, out.ctypes.data)
+    lib().vxo_field_doom(f.ctypes.data, X, Y, Z, (C.c_int * 7)(*plan), out.ctypes.data)
     return out
 
 

@@ -56,7 +56,7 @@ typedef struct {
                                  order only); a frame's flag VXO_FLAG_UNIT_GBUF does the same per frame */
     const uint8_t *held_doom; /* a doom table the caller built (vxo_field_doom) for the plan held_dplan
                                  (sx, sy, xlo, xhi, ylo, yhi), read instead of building one; NULL = none */
-    int held_dplan[6];
+    int held_dplan[7];
 } vxo_scene;
 
 /* Mirrors include/voxmap.h vx_frame_params field-for-field. */
@@ -99,26 +99,24 @@ typedef struct {
 #define VXO_FLAG_BLEND_FLOAT 0x10000u
 /* The sun doom table (DESIGN.md §3 "Doom table"), restated from the kernel's
  * launch_sun_doom: where a soft-shadow frame (shadow_samples >= 2) reads a
- * cone exit copy, a cell from which
- * every ray of the frame's sun samples provably enters a solid cell before
- * leaving the grid ends the march unlit at once when the march lands there
- * early enough (landing index j with j + (h + 1) * 2 * (kx + ky + 1) < MAX,
- * h = layers to the solid); later, the march goes on with the cell's texel and
- * no fetch is counted.  Only cells whose march texel is 1..VXO_DOOM_TMAX carry
- * it, and h <= VXO_DOOM_HMAX.  VXO_FLAG_NO_DOOM (= VX_FLAG_NO_DOOM) and
+ * cone exit copy, a cell from which every ray of the frame's sun samples
+ * provably enters a solid cell h layers up (h <= the plan's hmax) ends the
+ * march unlit at once when the march lands there early enough (landing index
+ * j with j + (h + 1) * 2 * (kx + ky + 1) < MAX); later, the march goes on with
+ * the cell's texel and no fetch is counted.  Only cells whose march texel is
+ * >= 1 carry it.  hmax = the largest h with (h + 1) 2 (kx + ky + 1) + 1 < MAX,
+ * at most VXO_DOOM_HCAP.  VXO_FLAG_NO_DOOM (= VX_FLAG_NO_DOOM) and
  * VX_FLAG_SOFT_BRICK frames read copies without it.  Frames are identical. */
 #define VXO_FLAG_NO_DOOM 0x20000u
 #define VXO_FLAG_SOFT_BRICK 0x100u
 #define VXO_DOOM_Q 4
-#define VXO_DOOM_HMAX 13
-#define VXO_DOOM_TMAX 8
-/* Sub-cell window of the frame's samples (all fast, one octant, r_z > 0): signs
- * sx, sy (+-1) and, per layer, the x / y sub-cell offsets [xlo, xhi], [ylo, yhi]
- * (Q = 4 sub-cells per cell, slack 1/64 cell). */
-void vxo_doom_plan(const float dirs[][3], int n, int *sx, int *sy, int *xlo, int *xhi, int *ylo, int *yhi);
-/* code[z][y][x] = h + 1 for doomed cells (h <= VXO_DOOM_HMAX), else 0 */
-void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, int sx, int sy, int xlo, int xhi, int ylo, int yhi,
-                    uint8_t *code);
+#define VXO_DOOM_HCAP 120
+/* plan = {sx, sy, xlo, xhi, ylo, yhi, hmax}: the sub-cell window of the
+ * frame's samples (all fast, one octant, r_z > 0), and hmax for its MAX and
+ * cone window kx, ky (hmax < 1: no table) */
+void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int kx, int ky, int plan[7]);
+/* code[z][y][x] = h + 1 for doomed cells (h <= plan[6]), else 0 */
+void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, const int plan[7], uint8_t *code);
 
 typedef struct {
     uint64_t pixels, sky_px, block_px, glass_px;

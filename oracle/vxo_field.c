@@ -294,8 +294,8 @@ void vxo_field_exit(const uint8_t *rgba, int X, int Y, int Z, int oct, int kx, i
  * (sub-cells outside the grid: inf).  A cell (x', y', z) not solid is doomed
  * with h = 1 + max over g' in [Q x' - 1, Q x' + Q + xhi] x [Q y' - 1, Q y' + Q
  * + yhi] of depth_{z+1}(g'): from anywhere in the cell a ray meets height z + 1
- * inside that window.  Depths saturate at 254 (inf = 255); h <= VXO_DOOM_HMAX. */
-void vxo_doom_plan(const float dirs[][3], int n, int *sx, int *sy, int *xlo, int *xhi, int *ylo, int *yhi) {
+ * inside that window.  Depths saturate at 254 (inf = 255); h <= the plan's hmax. */
+void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int kx, int ky, int plan[7]) {
     double axmin = 1e300, axmax = -1e300, aymin = 1e300, aymax = -1e300;
     for (int k = 0; k < n; k++) {
         const double ax = fabs((double)dirs[k][0] / (double)dirs[k][2]), ay = fabs((double)dirs[k][1] / (double)dirs[k][2]);
@@ -305,14 +305,17 @@ void vxo_doom_plan(const float dirs[][3], int n, int *sx, int *sy, int *xlo, int
         if (ay > aymax) aymax = ay;
     }
     const double eps = 1.0 / 64.0, Q = (double)VXO_DOOM_Q;
-    *sx = dirs[0][0] > 0.0f ? 1 : -1;
-    *sy = dirs[0][1] > 0.0f ? 1 : -1;
-    *xlo = (int)floor(Q * (axmin - eps)); *xhi = (int)ceil(Q * (axmax + eps));
-    *ylo = (int)floor(Q * (aymin - eps)); *yhi = (int)ceil(Q * (aymax + eps));
+    plan[0] = dirs[0][0] > 0.0f ? 1 : -1;
+    plan[1] = dirs[0][1] > 0.0f ? 1 : -1;
+    plan[2] = (int)floor(Q * (axmin - eps)); plan[3] = (int)ceil(Q * (axmax + eps));
+    plan[4] = (int)floor(Q * (aymin - eps)); plan[5] = (int)ceil(Q * (aymax + eps));
+    /* the stop rule j + (h + 1) dk2 < MAX can hold (at j = 1) only for h + 1 <= (MAX - 2) / dk2 */
+    const int dk2 = 2 * (kx + ky + 1), hm = max_steps >= 2 ? (max_steps - 2) / dk2 - 1 : -1;
+    plan[6] = hm < VXO_DOOM_HCAP ? hm : VXO_DOOM_HCAP;
 }
 
-void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, int sx, int sy, int xlo, int xhi, int ylo, int yhi,
-                    uint8_t *code) {
+void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, const int plan[7], uint8_t *code) {
+    const int sx = plan[0], sy = plan[1], xlo = plan[2], xhi = plan[3], ylo = plan[4], yhi = plan[5], hmax = plan[6];
     const int Q = VXO_DOOM_Q, GX = X * Q, GY = Y * Q;
     const size_t XY = (size_t)X * Y, G = (size_t)GX * GY;
     uint8_t *d1 = (uint8_t *)malloc(G), *d0 = (uint8_t *)malloc(G), *rx = (uint8_t *)malloc(G);
@@ -355,7 +358,7 @@ void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, int sx, int sy, in
                 const int h = m + 1;
                 const int xr = sx > 0 ? x : X - 1 - x, yr = sy > 0 ? y : Y - 1 - y;
                 code[(size_t)z * XY + (size_t)yr * X + xr] =
-                    (uint8_t)((m < 255 && h <= VXO_DOOM_HMAX && !VXO_SOLID(z, x, y)) ? h + 1 : 0);
+                    (uint8_t)((m < 255 && h <= hmax && !VXO_SOLID(z, x, y)) ? h + 1 : 0);
             }
         }
         /* states at height z */

@@ -210,7 +210,7 @@ static void white(const vxo_scene *s, float px, float py, float out[3]) {
  * without fetching it, as the kernel's march does on the -1 its table holds. */
 /* dm: the frame's doom table (vxo_field_doom, h + 1 per cell) or NULL; dk2 =
  * 2 (kx + ky + 1).  A march landing (index j) in a doomed cell whose march
- * texel T is 1..VXO_DOOM_TMAX ends unlit there, without a fetch, if j + (h + 1)
+ * texel T is >= 1 ends unlit there, without a fetch, if j + (h + 1)
  * dk2 < MAX: every ray of the window enters a solid cell h layers up and the
  * march lands on a zero texel on the way within (h + 1) dk2 landings (DESIGN.md
  * §3 "Doom table"); otherwise it goes on with safe = T, no fetch counted. */
@@ -254,7 +254,7 @@ static void march_ex(const vxo_scene *s, const int cell[3], const float fract[3]
         if (dm) {                                        /* doom table: unlit, no fetch (see above) */
             const size_t ci = (size_t)res->cell[0] + (size_t)s->X * ((size_t)res->cell[1] + (size_t)s->Y * res->cell[2]);
             const int T = s->field[4 * ci];              /* the march channel R (doom: r_z > 0) */
-            if (dm[ci] && T >= 1 && T <= VXO_DOOM_TMAX) {
+            if (dm[ci] && T >= 1) {
                 if (res->step + 1 + (int)dm[ci] * dk2 < max_steps) break;
                 safe = (float)T;
                 res->step++;
@@ -662,13 +662,15 @@ static void ctx_tables(shade_ctx *c) {
     const int cone = vxo_exit_plan((const float(*)[3])c->sun_dirs, c->n_sun, s->exit_mode == 1 && s->Z >= 3, oct,
                                    &kx, &ky);
     if (cone && c->n_sun > 1 && !(c->f->flags & (VXO_FLAG_NO_DOOM | VXO_FLAG_SOFT_BRICK))) {
-        int p[6];
-        vxo_doom_plan((const float(*)[3])c->sun_dirs, c->n_sun, &p[0], &p[1], &p[2], &p[3], &p[4], &p[5]);
-        if (s->held_doom && !memcmp(p, s->held_dplan, sizeof p)) {
+        int p[7];
+        vxo_doom_plan((const float(*)[3])c->sun_dirs, c->n_sun, c->max_steps, kx, ky, p);
+        if (p[6] < 1) {
+            /* no h can meet the stop rule at this MAX: no table */
+        } else if (s->held_doom && !memcmp(p, s->held_dplan, sizeof p)) {
             c->doom = s->held_doom;
         } else {
             c->doom_owned = (uint8_t *)malloc((size_t)s->X * s->Y * s->Z);
-            vxo_field_doom(s->field, s->X, s->Y, s->Z, p[0], p[1], p[2], p[3], p[4], p[5], c->doom_owned);
+            vxo_field_doom(s->field, s->X, s->Y, s->Z, p, c->doom_owned);
             c->doom = c->doom_owned;
         }
         c->doom_k2 = 2 * (kx + ky + 1);

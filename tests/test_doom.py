@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 NO_DOOM = 0x20000       # include/voxmap.h VX_FLAG_NO_DOOM (oracle/vxo.h VXO_FLAG_NO_DOOM)
-Q, EPS, HMAX = 4, 1.0 / 64.0, 13
+Q, EPS, HCAP = 4, 1.0 / 64.0, 120
 
 
 def _wmax(D, lo, hi, axis):
@@ -31,10 +31,12 @@ def _wmax(D, lo, hi, axis):
     return out
 
 
-def _doom_numpy(field, dirs):
+def _doom_numpy(field, dirs, max_steps, kx, ky):
     """Depth recursion over Q x Q sub-cells per cell, top layer down, in the
-    sun-aligned grid (x, y mirrored where the sun's component is negative)."""
+    sun-aligned grid (x, y mirrored where the sun's component is negative);
+    h up to the largest value the stop rule can use at landing 1."""
     d = np.asarray(dirs, np.float32).reshape(-1, 3)
+    hmax = min(HCAP, (max_steps - 2) // (2 * (kx + ky + 1)) - 1)
     ax = np.abs(d[:, 0].astype(np.float64) / d[:, 2].astype(np.float64))
     ay = np.abs(d[:, 1].astype(np.float64) / d[:, 2].astype(np.float64))
     xlo, xhi = math.floor(Q * (ax.min() - EPS)), math.ceil(Q * (ax.max() + EPS))
@@ -55,7 +57,7 @@ def _doom_numpy(field, dirs):
     for z in range(Z - 1, -1, -1):
         m = _wmax(_wmax(D1, -1, Q + xhi, 1), -1, Q + yhi, 0)[::Q, ::Q]
         h = m.astype(np.int32) + 1
-        code[z] = np.where((m < 255) & (h <= HMAX) & ~solid[z], h + 1, 0)
+        code[z] = np.where((m < 255) & (h <= hmax) & ~solid[z], h + 1, 0)
         s = solid[z]
 
         def cov(cy, cx):
@@ -68,7 +70,7 @@ def _doom_numpy(field, dirs):
         code = code[:, ::-1, :]
     if sx < 0:
         code = code[:, :, ::-1]
-    return np.ascontiguousarray(code), (sx, sy, xlo, xhi, ylo, yhi)
+    return np.ascontiguousarray(code), (sx, sy, xlo, xhi, ylo, yhi, hmax)
 
 
 def _sun(el_deg, az_deg):
@@ -90,12 +92,16 @@ def field(built):
 
 
 @pytest.mark.parametrize("el,az,radius,n", SUNS)
-def test_field_doom_matches_numpy_restatement(field, el, az, radius, n):
+@pytest.mark.parametrize("max_steps", [0, 200])
+def test_field_doom_matches_numpy_restatement(field, el, az, radius, n, max_steps):
     import oracle
     d = oracle.sun_samples(_sun(el, az), radius, n)
-    ref, plan = _doom_numpy(field, d)
-    assert oracle.doom_plan(d) == plan
-    got = oracle.field_doom(field, *plan)
+    cone, _, kx, ky = oracle.exit_plan(d)
+    assert cone
+    maxs = max_steps or 2 * field.shape[0]            # render.frag:12 (2 Z), or a frame's own
+    ref, plan = _doom_numpy(field, d, maxs, kx, ky)
+    assert oracle.doom_plan(d, maxs, kx, ky) == plan
+    got = oracle.field_doom(field, plan)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref), int((got != ref).sum())
     assert int((got > 0).sum()) > 0                       # the scene has doomed cells

@@ -37,7 +37,7 @@ struct vx_scene {
     struct Cone {
         int oct = -1, kx = -1, ky = -1;
         bool doom = false;            // the doom table is in (launch_sun_doom, window `plan`)
-        int plan[6] = {0, 0, 0, 0, 0, 0};
+        int plan[7] = {0, 0, 0, 0, 0, 0, 0};
         int8_t *d = nullptr;
         hipEvent_t ready = nullptr;   // recorded on the build's stream after the build
         unsigned long long used = 0;
@@ -434,7 +434,7 @@ struct TileSpec {
 // the build's first packet (vx_prepare_sun's timing), if built.
 // doom: the copy carries the doom table of window plan (DESIGN.md §3 "Doom
 // table"; part of the cache key).
-static int cone_copy(vx_scene *s, int oct, int kx, int ky, bool doom, const int plan[6], hipStream_t st,
+static int cone_copy(vx_scene *s, int oct, int kx, int ky, bool doom, const int plan[7], hipStream_t st,
                      const int8_t **out, bool *built, vx_scene::Cone **used, hipEvent_t t_build) {
     *built = false;
     vx_scene::Cone *slot = nullptr;
@@ -499,9 +499,9 @@ static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &
     if (tables && p->quality != 0 && !(p->flags & (VX_FLAG_NO_SHADOW | VX_FLAG_PRIMARY_ONLY))) {
         int oct, kx, ky;
         if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
-            const bool doom = fc.n_sun > 1 && !(p->flags & (VX_FLAG_NO_DOOM | VX_FLAG_SOFT_BRICK));
-            int plan[6] = {0, 0, 0, 0, 0, 0};
-            if (doom) doom_plan(fc, plan);
+            int plan[7] = {0, 0, 0, 0, 0, 0, 0};
+            doom_plan(fc, kx, ky, plan);
+            const bool doom = fc.n_sun > 1 && plan[6] >= 1 && !(p->flags & (VX_FLAG_NO_DOOM | VX_FLAG_SOFT_BRICK));
             const int rc = cone_copy(s, oct, kx, ky, doom, plan, st, sunc, &b, used, t_build);
             if (rc) return rc;
             if (doom && doom_k2) *doom_k2 = 2 * (kx + ky + 1);

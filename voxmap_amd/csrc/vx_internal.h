@@ -169,13 +169,16 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
 // The sun doom table (DESIGN.md §3 "Doom table", oracle vxo_field_doom): in a
 // cone copy already holding its exit marks and face bits, every cell from which
 // every ray of the sub-cell window {sx, sy, xlo, xhi, ylo, yhi} (doom_plan)
-// provably enters a solid cell h <= kDoomHMax layers up, and whose march texel
-// T is 1..kDoomTMax, becomes kDoomBase - (h * 8 + T - 1) (-11 .. -121).
-constexpr int kDoomQ = 4, kDoomHMax = 13, kDoomTMax = 8, kDoomBase = -10;
-int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[6], void *stream);
-// the doom table's window for a frame's samples (all fast, one octant, r_z > 0;
-// oracle vxo_doom_plan): sx, sy, then the per-layer sub-cell offsets xlo, xhi, ylo, yhi
-void doom_plan(const FrameConsts &fc, int plan[6]);
+// provably enters a solid cell h <= hmax layers up, and whose march texel is
+// >= 1, becomes kDoomBase - h (-9 .. -128); the march reads the texel itself
+// from the plain channel when it goes on from such a cell.
+constexpr int kDoomQ = 4, kDoomHCap = 120, kDoomBase = -8;
+int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[7], void *stream);
+// the doom table's plan for a frame's samples (all fast, one octant, r_z > 0)
+// and cone window kx, ky (oracle vxo_doom_plan): sx, sy, the per-layer
+// sub-cell offsets xlo, xhi, ylo, yhi, and hmax, the largest h whose stop rule
+// j + (h + 1) 2 (kx + ky + 1) < MAX_STEPS can hold (hmax < 1: no table)
+void doom_plan(const FrameConsts &fc, int kx, int ky, int plan[7]);
 // which copy a frame's sun march reads: 1 = one cone copy {oct, kx, ky} for every
 // sample (all on the fast path, one sign pattern, r_z > 0, slopes <= 4, kx, ky
 // <= SB); 0 = each fast sample its octant's orthant copy (oracle vxo_exit_plan)

@@ -499,12 +499,13 @@ __global__ void k_sun_cone_layer(const int8_t *ch, int8_t *out, int X, int Y, in
 // stages d1 over the sub-cells its windows reach (the cells' [4 x' - 1, 4 x' +
 // 4 + xhi] and the states' [gx + xlo, gx + xhi], xlo >= -1), takes the window
 // maxima separably in LDS (rows, then columns), writes d0 and turns each
-// doomed cell of the cone copy whose march texel T is 1..kDoomTMax into its
-// code.  Solid = R = G = 0 (sdf.cpp:430) inside the grid.
+// doomed cell (h <= hmax) of the cone copy whose march texel is >= 1 into
+// kDoomBase - h.  Solid = R = G = 0 (sdf.cpp:430) inside the grid.
 constexpr int kDoomT = 8, kDoomS = kDoomT * kDoomQ, kDoomW = kDoomS + 2 + 17 + 1;   // xhi <= 17 (|r_x / r_z| <= 4)
 __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t np, int8_t *sunc, const uint8_t *d1,
                                                     uint8_t *d0, int X, int Y, int z, int SB, int SXp, size_t SXpYp,
-                                                    int sx, int sy, int xlo, int xhi, int ylo, int yhi) {
+                                                    int sx, int sy, int xlo, int xhi, int ylo, int yhi,
+                                                    int hmax) {
     __shared__ uint8_t s_d[kDoomW][kDoomW];       // d1 rows H0 - 1 .., columns G0 - 1 ..
     __shared__ uint8_t s_rx[kDoomW][kDoomS];      // row maxima over the states' x windows
     __shared__ uint8_t s_rc[kDoomW][kDoomT];      // row maxima over the cells' x windows
@@ -562,10 +563,9 @@ __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t n
         if (xa < X && ya < Y && !s_solid[j + 1][i + 1]) {
             int m = 0;
             for (int r = kDoomQ * j; r <= kDoomQ * j + kDoomQ + 1 + yhi; r++) m = max(m, (int)s_rc[r][i]);
-            if (m < 255 && m + 1 <= kDoomHMax) {
+            if (m < 255 && m + 1 <= hmax) {
                 const size_t p = real(xa, ya);
-                const int t = sunc[p];
-                if (t >= 1 && t <= kDoomTMax) sunc[p] = (int8_t)(kDoomBase - (m * 8 + t - 1));
+                if (sunc[p] >= 1) sunc[p] = (int8_t)(kDoomBase - (m + 1));
             }
         }
     }
@@ -731,10 +731,11 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
     return (int)hipGetLastError();
 }
 
-int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[6], void *stream) {
-    const int sx = plan[0], sy = plan[1], xlo = plan[2], xhi = plan[3], ylo = plan[4], yhi = plan[5];
-    // the block's staged window (k_doom_layer): xlo, ylo >= -1, xhi, yhi <= 17
-    if (xlo < -1 || ylo < -1 || xhi > 17 || yhi > 17 || xlo > xhi || ylo > yhi || SB < 1)
+int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[7], void *stream) {
+    const int sx = plan[0], sy = plan[1], xlo = plan[2], xhi = plan[3], ylo = plan[4], yhi = plan[5], hmax = plan[6];
+    // the block's staged window (k_doom_layer): xlo, ylo >= -1, xhi, yhi <= 17; codes down to -128
+    if (xlo < -1 || ylo < -1 || xhi > 17 || yhi > 17 || xlo > xhi || ylo > yhi || SB < 1 || hmax < 1 ||
+        hmax > kDoomHCap)
         return (int)hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     const int SXp = X + 2 * SB, SYp = Y + 2 * SB, SZp = Z + 2 * SB;
@@ -749,7 +750,7 @@ int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
         const dim3 grid((unsigned)((X + kDoomT - 1) / kDoomT), (unsigned)((Y + kDoomT - 1) / kDoomT));
         for (int z = Z - 1, k = 0; z >= 0; z--, k ^= 1)
             hipLaunchKernelGGL(k_doom_layer, grid, dim3(256), 0, s, sunp, np, sunc, d[k], d[k ^ 1], X, Y, z, SB, SXp,
-                               SXpYp, sx, sy, xlo, xhi, ylo, yhi);
+                               SXpYp, sx, sy, xlo, xhi, ylo, yhi, hmax);
         e = hipGetLastError();
     }
     const hipError_t f = hipFreeAsync(d[0], s);

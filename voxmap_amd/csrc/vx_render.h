@@ -421,16 +421,16 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
 // offset terms, len = the first step's length (march_len_sg), rsrc = the
 // channel's typed-load descriptor (march_pad; march_soft shares these across
 // the samples of a fragment).
-// A doom code (soft-shadow frames' cone copies, launch_sun_doom) read at
-// landing j: the cell is one from which every ray of the frame's window meets
-// a solid cell h layers up, so the march lands on a 0 texel within (h + 1) 2
-// (kx + ky + 1) landings -- unlit (0) if that is before MAX_STEPS, else the
-// march goes on from the cell's texel T (oracle march_ex).  Anything else is
-// returned as read.
-__device__ __forceinline__ float doom_resolve(const KernelArgs &a, float t, int j, int maxs) {
-    if (t <= -9.5f) {
-        const int u = (int)(-10.0f - t);
-        t = j + ((u >> 3) + 2) * a.doom_k2 < maxs ? 0.0f : (float)((u & 7) + 1);
+// A doom code (soft-shadow frames' cone copies, launch_sun_doom: kDoomBase - h)
+// read at landing j: the cell is one from which every ray of the frame's window
+// meets a solid cell h layers up, so the march lands on a 0 texel within (h +
+// 1) 2 (kx + ky + 1) landings -- unlit (0) if that is before MAX_STEPS, else
+// the march goes on from the cell's texel T, read from the plain channel
+// (oracle march_ex).  Anything else is returned as read.
+__device__ __forceinline__ float doom_resolve(const KernelArgs &a, float t, int j, int maxs, unsigned off) {
+    if (t <= -8.5f) {
+        const int d = (int)(-7.0f - t);                                           // h + 1
+        t = j + d * a.doom_k2 < maxs ? 0.0f : ld_fmt1(buf_rsrc(a.sunp - 0x4B000000, kRsrcS8), off);
     }
     return t;
 }
@@ -458,13 +458,15 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
         exy += __builtin_fmaf(fl1, xpf, fl0); e2 += fl2;                          // :119 (exact)
         return __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy);
     };
+    // the offset of the cell the last step landed in
+    auto cell_off = [&]() -> unsigned { return __umul24(__float_as_uint(e2), sxpyp) + __float_as_uint(exy); };
     int step = 0;                                                                // wave-uniform
     const unsigned nl = active_lanes();
     if (maxs > 1) {                            // the first step, peeled: its len from march_len_sg
         float t = ld_fmt1(rsrc, advance());                                        // :123-128
         len = march_len_sg<SG>(S, f0, f1, f2);  // next step, under the load
         cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
-        if constexpr (DOOM) t = doom_resolve(a, t, 1, maxs);
+        if constexpr (DOOM) t = doom_resolve(a, t, 1, maxs, cell_off());
         tv = t;
         cnt.march_witers += once_per_wave(1u);
         cnt.march_slots += once_per_wave(nl);
@@ -482,15 +484,16 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
             cnt.march_slots += once_per_wave(nl);
         } while (tv > 0.0f && ++step < maxs - 1);
         if constexpr (DOOM) {
-            if (tv <= -9.5f) {                 // a doom code at landing j
-                tv = doom_resolve(a, tv, j, maxs);
+            if (tv <= -8.5f) {                 // a doom code at landing j
+                tv = doom_resolve(a, tv, j, maxs, cell_off());
                 while (tv > 0.0f && j < maxs - 1) {   // late: on from the cell's texel (rare)
-                    float t2 = ld_fmt1(rsrc, advance());
+                    const unsigned o = advance();
+                    const float t2 = ld_fmt1(rsrc, o);
                     len = march_len_fract<SG>(S, f0, f1, f2);
                     cnt.shadow_fetch += t2 >= 0.0f ? 1u : 0u;
                     cnt.march_witers += once_per_wave(1u);
                     cnt.march_slots += once_per_wave(nl);
-                    tv = doom_resolve(a, t2, ++j, maxs);
+                    tv = doom_resolve(a, t2, ++j, maxs, o);
                 }
             }
         }
