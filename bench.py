@@ -603,6 +603,17 @@ def main(argv=None):
         marched5 = rays5 - s5["shadow_rays_resolved"]
         ms5 = 1000.0 * b["wall_s"] / n5
         ach5, frac5 = roofline_of(s5["alg_bytes"], b["ev_ms"])
+        # the same frame's bytes without the sun doom table (DESIGN.md §3 "Doom table":
+        # the table skips fetches of marches that end unlit anyway, so the frame's own
+        # bytes fall with its time); that march's bytes over this frame's time
+        f5n = vx.Frame(f5.params.copy(), c5cfg["w"], c5cfg["h"])
+        f5n.params.flags |= vx.FLAG_NO_DOOM
+        o5 = torch.empty(c5cfg["w"] * c5cfg["h"] * 4, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        s5n = sc5.render_device(f5n, o5.data_ptr(), pixel_format=vx.PIXEL_RGBA8, stats=True).as_dict()
+        torch.cuda.synchronize()
+        del o5
+        frac5n = roofline_of(s5n["alg_bytes"], b["ev_ms"])[1]
         t5j = pmc_entry(f"traffic_{PMC_TAG}_c5.json", "C5", c5cfg["camera"], flags, c5cfg["samples"])
         c5 = {"workload": f"C5: {c5cfg['w']}x{c5cfg['h']}, field {X5}x{Y5}x{Z5} (S-proc 3x nearest upsample), "
                           f"full quality + {c5cfg['samples']}-sample soft shadows (sun radius {args.sun_radius})",
@@ -615,6 +626,7 @@ def main(argv=None):
               "single_stream_ms_per_frame": round(b["ev_ms"], 4),
               "alg_bytes": int(s5["alg_bytes"]), "roofline_achieved_gbps": round(ach5, 2),
               "roofline_frac": round(frac5, 4), "traffic": t5j.get("hbm_bytes_per_launch") if t5j else None,
+              "alg_bytes_no_doom": int(s5n["alg_bytes"]), "roofline_frac_no_doom_bytes": round(frac5n, 4),
               "lane_util": lane_utils(s5), "scene_build_s": round(t5, 3), "frames": n5, "timing": b["blocks"],
               "exit_tables": b["exit"]}
         sc5.close()

@@ -283,7 +283,7 @@ void vxo_field_exit(const uint8_t *rgba, int X, int Y, int Z, int oct, int kx, i
 /* ---------------- the sun doom table (DESIGN.md §3 "Doom table") ----------------
  * In sun-aligned coordinates (x', y' grow toward the sun: x' = x if sx > 0,
  * else X - 1 - x), a ray of the frame's samples rises one layer while x' grows
- * by a slope in [ax_min, ax_max] (y' likewise).  Q = 4 sub-cells per cell and
+ * by a slope in [ax_min, ax_max] (y' likewise).  Q = VXO_DOOM_Q sub-cells per cell and
  * axis.  State S_z(g) (g a sub-cell (gx, gy) at height z, the bottom of layer
  * z): every ray crossing height z inside g (within 1/64 cell) enters a solid
  * cell (R = G = 0, sdf.cpp:430) before leaving the grid; depth(g) = layers to

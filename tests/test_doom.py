@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 NO_DOOM = 0x20000       # include/voxmap.h VX_FLAG_NO_DOOM (oracle/vxo.h VXO_FLAG_NO_DOOM)
-Q, EPS, HCAP = 4, 1.0 / 64.0, 120
+Q, EPS, HCAP = 8, 1.0 / 64.0, 120
 
 
 def _wmax(D, lo, hi, axis):

@@ -172,7 +172,7 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
 // provably enters a solid cell h <= hmax layers up, and whose march texel is
 // >= 1, becomes kDoomBase - h (-9 .. -128); the march reads the texel itself
 // from the plain channel when it goes on from such a cell.
-constexpr int kDoomQ = 4, kDoomHCap = 120, kDoomBase = -8;
+constexpr int kDoomQ = 8, kDoomHCap = 120, kDoomBase = -8;
 int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[7], void *stream);
 // the doom table's plan for a frame's samples (all fast, one octant, r_z > 0)
 // and cone window kx, ky (oracle vxo_doom_plan): sx, sy, the per-layer

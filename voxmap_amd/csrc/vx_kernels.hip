@@ -495,13 +495,14 @@ __global__ void k_sun_cone_layer(const int8_t *ch, int8_t *out, int X, int Y, in
 // ---- one layer z of the sun doom table (oracle vxo_field_doom; DESIGN.md §3
 // "Doom table"), sun-aligned coordinates (x' = x if sx > 0, else X - 1 - x).
 // d1 = the sub-cell states at height z + 1 (GX x GY, 255 = leaves the grid),
-// d0 = those at height z.  A block takes 8 x 8 cells = 32 x 32 sub-cells: it
+// d0 = those at height z.  A block takes 8 x 8 cells = 8Q x 8Q sub-cells: it
 // stages d1 over the sub-cells its windows reach (the cells' [4 x' - 1, 4 x' +
 // 4 + xhi] and the states' [gx + xlo, gx + xhi], xlo >= -1), takes the window
 // maxima separably in LDS (rows, then columns), writes d0 and turns each
 // doomed cell (h <= hmax) of the cone copy whose march texel is >= 1 into
 // kDoomBase - h.  Solid = R = G = 0 (sdf.cpp:430) inside the grid.
-constexpr int kDoomT = 8, kDoomS = kDoomT * kDoomQ, kDoomW = kDoomS + 2 + 17 + 1;   // xhi <= 17 (|r_x / r_z| <= 4)
+// xhi <= ceil(Q (4 + 1/64)) = 4 Q + 1 (cone plans: |r_x / r_z| <= 4)
+constexpr int kDoomT = 8, kDoomS = kDoomT * kDoomQ, kDoomXhi = 4 * kDoomQ + 1, kDoomW = kDoomS + 2 + kDoomXhi + 1;
 __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t np, int8_t *sunc, const uint8_t *d1,
                                                     uint8_t *d0, int X, int Y, int z, int SB, int SXp, size_t SXpYp,
                                                     int sx, int sy, int xlo, int xhi, int ylo, int yhi,
@@ -733,8 +734,8 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
 
 int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[7], void *stream) {
     const int sx = plan[0], sy = plan[1], xlo = plan[2], xhi = plan[3], ylo = plan[4], yhi = plan[5], hmax = plan[6];
-    // the block's staged window (k_doom_layer): xlo, ylo >= -1, xhi, yhi <= 17; codes down to -128
-    if (xlo < -1 || ylo < -1 || xhi > 17 || yhi > 17 || xlo > xhi || ylo > yhi || SB < 1 || hmax < 1 ||
+    // the block's staged window (k_doom_layer): xlo, ylo >= -1, xhi, yhi <= kDoomXhi; codes down to -128
+    if (xlo < -1 || ylo < -1 || xhi > kDoomXhi || yhi > kDoomXhi || xlo > xhi || ylo > yhi || SB < 1 || hmax < 1 ||
         hmax > kDoomHCap)
         return (int)hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
