@@ -125,6 +125,18 @@ def test_doom_frames_identical_with_fewer_fetches(field, noise):
         assert sa.as_dict()["shadow_rays"] == sb.as_dict()["shadow_rays"]
         saved += fb - fa
     assert saved > 0
+    # short budgets: codes resolved late go on from the texel; no table when no h fits
+    for maxs in (12, 20, 30):
+        for el, az, radius, n in SUNS[:3]:
+            fa = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(el, az),
+                               flags=vx.FLAG_FULL_QUALITY, shadow_samples=n, sun_radius=radius, max_shadow_steps=maxs)
+            fb = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(el, az),
+                               flags=vx.FLAG_FULL_QUALITY | NO_DOOM, shadow_samples=n, sun_radius=radius,
+                               max_shadow_steps=maxs)
+            ia, sa = o.render(fa.params, 96, 64)
+            ib, sb = o.render(fb.params, 96, 64)
+            assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32)), (maxs, el, az)
+            assert sa.as_dict()["shadow_fetches"] <= sb.as_dict()["shadow_fetches"]
     # the hard shadow has no doom rule: a one-sample frame counts the same fetches either way
     a = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(15, 45), flags=vx.FLAG_FULL_QUALITY)
     b = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(15, 45),

@@ -77,6 +77,30 @@ def test_doom_frames_and_counters_equal_the_oracle(small, noise, el, az, radius,
     assert got[0][1] <= got[vx.FLAG_NO_DOOM][1]
 
 
+@pytest.mark.parametrize("max_steps", [12, 20, 30, 44])
+def test_doom_step_budgets(small, noise, max_steps):
+    """Short march budgets (max_shadow_steps): hmax shrinks with MAX, a code read
+    late in a march goes on from the cell's texel (read from the plain channel),
+    and a budget too short for any h builds no table; frames and counters equal
+    the oracle's, frames equal the no-doom frames."""
+    import oracle
+    import voxmap_amd as vx
+    sc, _ = small
+    o = oracle.Oracle(sc.read_field(), noise, exit=True)
+    for el, az, radius, n in SUNS[:7]:
+        got = []
+        for fl in (0, vx.FLAG_NO_DOOM):
+            fr = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(el, az),
+                               flags=vx.FLAG_FULL_QUALITY | fl, shadow_samples=n, sun_radius=radius,
+                               max_shadow_steps=max_steps)
+            img, st = sc.render(fr, stats=True)
+            ref, ost = o.render(fr.params, 96, 64)
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (el, az, fl)
+            assert st.as_dict()["shadow_fetches"] == ost.as_dict()["shadow_fetches"], (el, az, fl)
+            got.append(img)
+        assert np.array_equal(got[0].view(np.uint32), got[1].view(np.uint32))
+
+
 def test_soft_brick_frames_read_no_doom_codes(small, noise):
     """VX_FLAG_SOFT_BRICK frames read a cone copy without the table (its LDS
     brick march has no doom rule): same frame as the default, counters equal

@@ -495,14 +495,18 @@ __global__ void k_sun_cone_layer(const int8_t *ch, int8_t *out, int X, int Y, in
 // ---- one layer z of the sun doom table (oracle vxo_field_doom; DESIGN.md §3
 // "Doom table"), sun-aligned coordinates (x' = x if sx > 0, else X - 1 - x).
 // d1 = the sub-cell states at height z + 1 (GX x GY, 255 = leaves the grid),
-// d0 = those at height z.  A block takes 8 x 8 cells = 8Q x 8Q sub-cells: it
-// stages d1 over the sub-cells its windows reach (the cells' [4 x' - 1, 4 x' +
-// 4 + xhi] and the states' [gx + xlo, gx + xhi], xlo >= -1), takes the window
-// maxima separably in LDS (rows, then columns), writes d0 and turns each
-// doomed cell (h <= hmax) of the cone copy whose march texel is >= 1 into
-// kDoomBase - h.  Solid = R = G = 0 (sdf.cpp:430) inside the grid.
+// d0 = those at height z.  A block (4 waves) takes 8 x 8 cells = 64 x 64
+// sub-cells, one sub-cell column per lane: it stages d1 over the sub-cells its
+// windows reach (the cells' [Q x' - 1, Q x' + Q + xhi] and the states' [gx +
+// xlo, gx + xhi], xlo >= -1) in LDS, takes the window maxima separably (rows
+// per wave; a cell's wide row window split over 8 lanes and joined by lane
+// shuffles), writes d0 and turns each doomed cell (h <= hmax) of the cone copy
+// whose march texel is >= 1 into kDoomBase - h.  Solid = R = G = 0
+// (sdf.cpp:430) inside the grid.  No integer division: every loop walks rows
+// by wave and columns by lane.
 // xhi <= ceil(Q (4 + 1/64)) = 4 Q + 1 (cone plans: |r_x / r_z| <= 4)
 constexpr int kDoomT = 8, kDoomS = kDoomT * kDoomQ, kDoomXhi = 4 * kDoomQ + 1, kDoomW = kDoomS + 2 + kDoomXhi + 1;
+static_assert(kDoomS == 64 && kDoomQ == 8, "k_doom_layer maps one sub-cell column to each lane of a wave");
 __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t np, int8_t *sunc, const uint8_t *d1,
                                                     uint8_t *d0, int X, int Y, int z, int SB, int SXp, size_t SXpYp,
                                                     int sx, int sy, int xlo, int xhi, int ylo, int yhi,
@@ -515,18 +519,37 @@ __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t n
     const int x0 = blockIdx.x * kDoomT, y0 = blockIdx.y * kDoomT;          // aligned cells
     const int G0 = x0 * kDoomQ, H0 = y0 * kDoomQ;
     const int W = kDoomS + 2 + xhi, H = kDoomS + 2 + yhi;
-    const int tid = threadIdx.x;
-    for (int k = tid; k < W * H; k += 256) {
-        const int r = k / W, c = k - r * W;
-        const int gx = G0 - 1 + c, gy = H0 - 1 + r;
-        s_d[r][c] = (gx < 0 || gx >= GX || gy < 0 || gy >= GY) ? (uint8_t)255 : d1[(size_t)gy * GX + gx];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    {
+        // every load of the wave's rows issued before the first LDS write (a
+        // load-store pair per row kept one load in flight: 735 us a layer at C5)
+        constexpr int kRows = (kDoomW + 3) / 4;
+        uint32_t v[kRows];
+#pragma unroll
+        for (int k = 0; k < kRows; k++) {
+            const int r = wv + 4 * k, gy = H0 - 1 + r;
+            const bool rowin = r < H && gy >= 0 && gy < GY;
+            const uint8_t *row = d1 + (size_t)(rowin ? gy : 0) * GX;
+            const int g0 = G0 - 1 + lane, g1 = g0 + 64;
+            const uint32_t a0 = (rowin && g0 >= 0 && g0 < GX) ? row[g0] : 255u;
+            const uint32_t a1 = (rowin && lane + 64 < W && g1 < GX) ? row[g1] : 255u;
+            v[k] = a0 | (a1 << 8);
+        }
+#pragma unroll
+        for (int k = 0; k < kRows; k++) {
+            const int r = wv + 4 * k;
+            if (r < H) {
+                s_d[r][lane] = (uint8_t)(v[k] & 0xffu);
+                if (lane + 64 < W) s_d[r][lane + 64] = (uint8_t)(v[k] >> 8);
+            }
+        }
     }
     auto real = [&](int xa, int ya) {            // padded offset of aligned cell (xa, ya, z)
         const int xr = sx > 0 ? xa : X - 1 - xa, yr = sy > 0 ? ya : Y - 1 - ya;
         return (size_t)(xr + SB) + (size_t)SXp * (size_t)(yr + SB) + SXpYp * (size_t)(z + SB);
     };
-    if (tid < (kDoomT + 2) * (kDoomT + 2)) {
-        const int j = tid / (kDoomT + 2), i = tid - j * (kDoomT + 2);
+    if (threadIdx.x < (kDoomT + 2) * (kDoomT + 2)) {
+        const int j = threadIdx.x / (kDoomT + 2), i = threadIdx.x - j * (kDoomT + 2);   // constant divisor
         const int xa = x0 - 1 + i, ya = y0 - 1 + j;
         bool solid = false;
         if (xa >= 0 && xa < X && ya >= 0 && ya < Y) {
@@ -536,30 +559,38 @@ __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t n
         s_solid[j][i] = solid ? 1 : 0;
     }
     __syncthreads();
-    for (int k = tid; k < H * (kDoomS + kDoomT); k += 256) {
-        const int r = k / (kDoomS + kDoomT), c = k - r * (kDoomS + kDoomT);
-        int lo, hi;
-        if (c < kDoomS) { lo = c + 1 + xlo; hi = c + 1 + xhi; }            // sub-cell G0 + c
-        else { lo = kDoomQ * (c - kDoomS); hi = lo + kDoomQ + 1 + xhi; }    // cell x0 + (c - kDoomS)
+    // rows: lane c the state window [c + 1 + xlo, c + 1 + xhi]; the cells' windows
+    // [Q i, Q i + Q + 1 + xhi] as 8 lanes per cell (lane = 8 i + p reads Q i + p + 8 k)
+    const int ci = lane >> 3, cp = lane & 7, chi = kDoomQ * ci + kDoomQ + 1 + xhi;
+    for (int r = wv; r < H; r += 4) {
         int m = 0;
-        for (int q = lo; q <= hi; q++) m = max(m, (int)s_d[r][q]);
-        if (c < kDoomS) s_rx[r][c] = (uint8_t)m; else s_rc[r][c - kDoomS] = (uint8_t)m;
+        for (int q = lane + 1 + xlo; q <= lane + 1 + xhi; q++) m = max(m, (int)s_d[r][q]);
+        s_rx[r][lane] = (uint8_t)m;
+        int mc = 0;
+        for (int q = kDoomQ * ci + cp; q <= chi; q += 8) mc = max(mc, (int)s_d[r][q]);
+        mc = max(mc, __shfl_xor(mc, 1));
+        mc = max(mc, __shfl_xor(mc, 2));
+        mc = max(mc, __shfl_xor(mc, 4));
+        if (cp == 0) s_rc[r][ci] = (uint8_t)mc;
     }
     __syncthreads();
-    for (int k = tid; k < kDoomS * kDoomS; k += 256) {                     // states at height z
-        const int j = k / kDoomS, i = k - j * kDoomS;
-        const int gx = G0 + i, gy = H0 + j;
-        if (gx >= GX || gy >= GY) continue;
-        int m = 0;
-        for (int r = j + 1 + ylo; r <= j + 1 + yhi; r++) m = max(m, (int)s_rx[r][i]);
-        const int ci = i / kDoomQ, a = i % kDoomQ, cj = j / kDoomQ, b = j % kDoomQ;
-        const int xa0 = ci + 1 - (a == 0 ? 1 : 0), xa1 = ci + 1 + (a == kDoomQ - 1 ? 1 : 0);   // in s_solid
-        const int ya0 = cj + 1 - (b == 0 ? 1 : 0), ya1 = cj + 1 + (b == kDoomQ - 1 ? 1 : 0);
-        const bool es = s_solid[ya0][xa0] && s_solid[ya0][xa1] && s_solid[ya1][xa0] && s_solid[ya1][xa1];
-        d0[(size_t)gy * GX + gx] = (uint8_t)(es ? 0 : (m < 255 ? min(m + 1, 254) : 255));
+    {                                                                        // states at height z
+        const int i = lane, gx = G0 + i;
+        const int cx = i >> 3, a = i & 7;
+        const int xa0 = cx + 1 - (a == 0 ? 1 : 0), xa1 = cx + 1 + (a == kDoomQ - 1 ? 1 : 0);   // in s_solid
+        for (int j = wv; j < kDoomS; j += 4) {
+            const int gy = H0 + j;
+            if (gx >= GX || gy >= GY) continue;
+            int m = 0;
+            for (int r = j + 1 + ylo; r <= j + 1 + yhi; r++) m = max(m, (int)s_rx[r][i]);
+            const int cj = j >> 3, b = j & 7;
+            const int ya0 = cj + 1 - (b == 0 ? 1 : 0), ya1 = cj + 1 + (b == kDoomQ - 1 ? 1 : 0);
+            const bool es = s_solid[ya0][xa0] && s_solid[ya0][xa1] && s_solid[ya1][xa0] && s_solid[ya1][xa1];
+            d0[(size_t)gy * GX + gx] = (uint8_t)(es ? 0 : (m < 255 ? min(m + 1, 254) : 255));
+        }
     }
-    if (tid < kDoomT * kDoomT) {                                            // cells of layer z
-        const int j = tid / kDoomT, i = tid - j * kDoomT;
+    if (threadIdx.x < kDoomT * kDoomT) {                                    // cells of layer z (wave 0)
+        const int j = threadIdx.x >> 3, i = threadIdx.x & 7;
         const int xa = x0 + i, ya = y0 + j;
         if (xa < X && ya < Y && !s_solid[j + 1][i + 1]) {
             int m = 0;
