@@ -109,7 +109,7 @@ typedef struct {
  * VX_FLAG_SOFT_BRICK frames read copies without it.  Frames are identical. */
 #define VXO_FLAG_NO_DOOM 0x20000u
 #define VXO_FLAG_SOFT_BRICK 0x100u
-#define VXO_DOOM_Q 8
+#define VXO_DOOM_Q 8     /* <= 9: the margin 1/Q the stop rule needs (DESIGN.md §3 "Doom table") */
 #define VXO_DOOM_HCAP 120
 /* plan = {sx, sy, xlo, xhi, ylo, yhi, hmax}: the sub-cell window of the
  * frame's samples (all fast, one octant, r_z > 0), and hmax for its MAX and

@@ -173,6 +173,10 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
 // >= 1, becomes kDoomBase - h (-9 .. -128); the march reads the texel itself
 // from the plain channel when it goes on from such a cell.
 constexpr int kDoomQ = 8, kDoomHCap = 120, kDoomBase = -8;
+// the stop rule's soundness: a march step ends within 0.1024 cell of where its
+// segment entered the doomed ray's solid region (T = 1, |r_a| >= 2^-10), inside
+// the 1/Q margin the recursion checks (DESIGN.md §3 "Doom table", the stop rule)
+static_assert(kDoomQ <= 9, "doom margin 1/Q must exceed the 0.1024-cell step overshoot plus drift");
 int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[7], void *stream);
 // the doom table's plan for a frame's samples (all fast, one octant, r_z > 0)
 // and cone window kx, ky (oracle vxo_doom_plan): sx, sy, the per-layer
