@@ -89,7 +89,7 @@ def lib():
         L.vxo_exit_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_int)]
         L.vxo_exit_plan.restype = C.c_int
-        L.vxo_doom_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+        L.vxo_doom_plan.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int)]
         L.vxo_doom_plan.restype = None
         L.vxo_field_doom.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_void_p]
         L.vxo_field_doom.restype = None
@@ -167,7 +167,7 @@ class Oracle:
         self.sc.held_oct, self.sc.held_kx, self.sc.held_ky = octs[0], kx, ky
         if cone and len(d) > 1 and not (params.flags & (0x20000 | 0x100)):   # soft shadows: the doom table
             Z = self.sc.Z
-            plan = doom_plan(d, params.max_shadow_steps if params.max_shadow_steps > 0 else 2 * Z, kx, ky)
+            plan = doom_plan(d, params.max_shadow_steps if params.max_shadow_steps > 0 else 2 * Z)
             if plan[6] >= 1:
                 self._held_doom = field_doom(self.field, plan)
                 self.sc.held_doom = self._held_doom.ctypes.data
@@ -305,20 +305,20 @@ def field_exit(field_zyx4: np.ndarray, oct: int, kx: int = -1, ky: int = -1) -> 
     return out
 
 
-def doom_plan(dirs, max_steps: int, kx: int, ky: int):
+def doom_plan(dirs, max_steps: int):
     """(sx, sy, xlo, xhi, ylo, yhi, hmax): the doom table's sub-cell window for
     a frame's sun samples (vxo_doom_plan; all fast, one octant, r_z > 0) and the
-    largest h its stop rule can use at MAX = max_steps with cone window kx, ky."""
+    largest h its stop rule can use at MAX = max_steps."""
     d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
     v = (C.c_int * 7)()
-    lib().vxo_doom_plan(d.ctypes.data, d.shape[0], int(max_steps), int(kx), int(ky), v)
+    lib().vxo_doom_plan(d.ctypes.data, d.shape[0], int(max_steps), v)
     return tuple(v)
 
 
 def field_doom(field_zyx4: np.ndarray, plan) -> np.ndarray:
-    """(Z, Y, X) uint8: the sun doom table (vxo_field_doom): h + 1
-    where every ray of the window provably enters a solid cell h <= hmax layers
-    up, else 0."""
+    """(Z, Y, X) uint8: the sun doom table (vxo_field_doom): the
+    crossing bound C(h) where every ray of the window provably enters a solid
+    cell h <= hmax layers up, else 0."""
     f = np.ascontiguousarray(field_zyx4, np.uint8)
     Z, Y, X, _ = f.shape
     out = np.empty((Z, Y, X), np.uint8)

@@ -102,20 +102,23 @@ typedef struct {
  * cone exit copy, a cell from which every ray of the frame's sun samples
  * provably enters a solid cell h layers up (h <= the plan's hmax) ends the
  * march unlit at once when the march lands there early enough (landing index
- * j with j + (h + 1) * 2 * (kx + ky + 1) < MAX); later, the march goes on with
+ * j with j + 2 C < MAX, C = vxo_doom_cross(h)); later, the march goes on with
  * the cell's texel and no fetch is counted.  Only cells whose march texel is
- * >= 1 carry it.  hmax = the largest h with (h + 1) 2 (kx + ky + 1) + 1 < MAX,
- * at most VXO_DOOM_HCAP.  VXO_FLAG_NO_DOOM (= VX_FLAG_NO_DOOM) and
+ * >= 1 carry it.  hmax = the largest h with 1 + 2 C(h) < MAX and C(h) <=
+ * VXO_DOOM_HCAP (the kernel's int8 codes).  VXO_FLAG_NO_DOOM (= VX_FLAG_NO_DOOM) and
  * VX_FLAG_SOFT_BRICK frames read copies without it.  Frames are identical. */
 #define VXO_FLAG_NO_DOOM 0x20000u
 #define VXO_FLAG_SOFT_BRICK 0x100u
 #define VXO_DOOM_Q 8     /* <= 9: the margin 1/Q the stop rule needs (DESIGN.md §3 "Doom table") */
 #define VXO_DOOM_HCAP 120
 /* plan = {sx, sy, xlo, xhi, ylo, yhi, hmax}: the sub-cell window of the
- * frame's samples (all fast, one octant, r_z > 0), and hmax for its MAX and
- * cone window kx, ky (hmax < 1: no table) */
-void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int kx, int ky, int plan[7]);
-/* code[z][y][x] = h + 1 for doomed cells (h <= plan[6]), else 0 */
+ * frame's samples (all fast, one octant, r_z > 0), and hmax for its MAX
+ * (hmax < 1: no table) */
+void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int plan[7]);
+/* the boundary crossings a march makes from a doomed cell with h into its
+ * block: h in z, floor(h xhi / Q) + 1 in x, floor(h yhi / Q) + 1 in y */
+int vxo_doom_cross(int h, int xhi, int yhi);
+/* code[z][y][x] = vxo_doom_cross(h, ...) for doomed cells (h <= plan[6]), else 0 */
 void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, const int plan[7], uint8_t *code);
 
 typedef struct {

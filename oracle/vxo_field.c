@@ -295,7 +295,11 @@ void vxo_field_exit(const uint8_t *rgba, int X, int Y, int Z, int oct, int kx, i
  * with h = 1 + max over g' in [Q x' - 1, Q x' + Q + xhi] x [Q y' - 1, Q y' + Q
  * + yhi] of depth_{z+1}(g'): from anywhere in the cell a ray meets height z + 1
  * inside that window.  Depths saturate at 254 (inf = 255); h <= the plan's hmax. */
-void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int kx, int ky, int plan[7]) {
+int vxo_doom_cross(int h, int xhi, int yhi) {
+    return h + (h * xhi) / VXO_DOOM_Q + 1 + (h * yhi) / VXO_DOOM_Q + 1;
+}
+
+void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int plan[7]) {
     double axmin = 1e300, axmax = -1e300, aymin = 1e300, aymax = -1e300;
     for (int k = 0; k < n; k++) {
         const double ax = fabs((double)dirs[k][0] / (double)dirs[k][2]), ay = fabs((double)dirs[k][1] / (double)dirs[k][2]);
@@ -309,9 +313,12 @@ void vxo_doom_plan(const float dirs[][3], int n, int max_steps, int kx, int ky, 
     plan[1] = dirs[0][1] > 0.0f ? 1 : -1;
     plan[2] = (int)floor(Q * (axmin - eps)); plan[3] = (int)ceil(Q * (axmax + eps));
     plan[4] = (int)floor(Q * (aymin - eps)); plan[5] = (int)ceil(Q * (aymax + eps));
-    /* the stop rule j + (h + 1) dk2 < MAX can hold (at j = 1) only for h + 1 <= (MAX - 2) / dk2 */
-    const int dk2 = 2 * (kx + ky + 1), hm = max_steps >= 2 ? (max_steps - 2) / dk2 - 1 : -1;
-    plan[6] = hm < VXO_DOOM_HCAP ? hm : VXO_DOOM_HCAP;
+    /* the stop rule j + 2 C(h) < MAX can hold (at j = 1) only for 1 + 2 C(h) < MAX; C grows with h */
+    int hm = 0;
+    while (hm < VXO_DOOM_HCAP && vxo_doom_cross(hm + 1, plan[3], plan[5]) <= VXO_DOOM_HCAP &&
+           1 + 2 * vxo_doom_cross(hm + 1, plan[3], plan[5]) < max_steps)
+        hm++;
+    plan[6] = hm;
 }
 
 void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, const int plan[7], uint8_t *code) {
@@ -358,7 +365,7 @@ void vxo_field_doom(const uint8_t *rgba, int X, int Y, int Z, const int plan[7],
                 const int h = m + 1;
                 const int xr = sx > 0 ? x : X - 1 - x, yr = sy > 0 ? y : Y - 1 - y;
                 code[(size_t)z * XY + (size_t)yr * X + xr] =
-                    (uint8_t)((m < 255 && h <= hmax && !VXO_SOLID(z, x, y)) ? h + 1 : 0);
+                    (uint8_t)((m < 255 && h <= hmax && !VXO_SOLID(z, x, y)) ? vxo_doom_cross(h, xhi, yhi) : 0);
             }
         }
         /* states at height z */

@@ -208,15 +208,16 @@ static void white(const vxo_scene *s, float px, float py, float out[3]) {
 /* ex: the build's exit table for this direction (vxo_exit_plan), or NULL for
  * the reference's literal march.  A march entering a flagged cell ends "lit"
  * without fetching it, as the kernel's march does on the -1 its table holds. */
-/* dm: the frame's doom table (vxo_field_doom, h + 1 per cell) or NULL; dk2 =
- * 2 (kx + ky + 1).  A march landing (index j) in a doomed cell whose march
- * texel T is >= 1 ends unlit there, without a fetch, if j + (h + 1)
- * dk2 < MAX: every ray of the window enters a solid cell h layers up and the
- * march lands on a zero texel on the way within (h + 1) dk2 landings (DESIGN.md
- * §3 "Doom table"); otherwise it goes on with safe = T, no fetch counted. */
+/* dm: the frame's doom table (vxo_field_doom: C, the crossings to the block,
+ * per doomed cell) or NULL.  A march landing (index j) in a doomed cell whose
+ * march texel T is >= 1 ends unlit there, without a fetch, if j + 2 C < MAX:
+ * every ray of the window enters a solid cell h layers up after at most C
+ * boundary crossings, and the march crosses one at least every two landings
+ * (DESIGN.md §3 "Doom table"); otherwise it goes on with safe = T, no fetch
+ * counted. */
 static void march_ex(const vxo_scene *s, const int cell[3], const float fract[3],
                      const float r[3], int max_steps, vxo_march_t *res, const uint8_t *ex,
-                     const uint8_t *dm, int dk2) {
+                     const uint8_t *dm) {
     res->step = 0;
     res->fetches = 0;
     res->cell[0] = cell[0]; res->cell[1] = cell[1]; res->cell[2] = cell[2];
@@ -255,7 +256,7 @@ static void march_ex(const vxo_scene *s, const int cell[3], const float fract[3]
             const size_t ci = (size_t)res->cell[0] + (size_t)s->X * ((size_t)res->cell[1] + (size_t)s->Y * res->cell[2]);
             const int T = s->field[4 * ci];              /* the march channel R (doom: r_z > 0) */
             if (dm[ci] && T >= 1) {
-                if (res->step + 1 + (int)dm[ci] * dk2 < max_steps) break;
+                if (res->step + 1 + 2 * (int)dm[ci] < max_steps) break;
                 safe = (float)T;
                 res->step++;
                 continue;
@@ -272,7 +273,7 @@ static void march_ex(const vxo_scene *s, const int cell[3], const float fract[3]
 
 void vxo_march(const vxo_scene *s, const int cell[3], const float fract[3],
                const float r[3], int max_steps, vxo_march_t *res) {
-    march_ex(s, cell, fract, r, max_steps, res, NULL, NULL, 0);
+    march_ex(s, cell, fract, r, max_steps, res, NULL, NULL);
 }
 
 /* The build's choice of exit table per sample (DESIGN.md §3 "Sun exit
@@ -637,7 +638,6 @@ typedef struct {
     int n_owned;
     const uint8_t *doom;                     /* the cone plan's doom table (vxo_field_doom), else NULL */
     uint8_t *doom_owned;
-    int doom_k2;                             /* 2 (kx + ky + 1) */
 } shade_ctx;
 
 static void ctx_init(shade_ctx *c, const vxo_scene *s, const vxo_frame *f) {
@@ -650,7 +650,6 @@ static void ctx_init(shade_ctx *c, const vxo_scene *s, const vxo_frame *f) {
     for (int k = 0; k < VXO_MAX_SAMPLES; k++) c->ex[k] = NULL;
     c->doom = NULL;
     c->doom_owned = NULL;
-    c->doom_k2 = 0;
 }
 
 /* the frame's exit tables (vxo_render only: a table is a pass over the field) */
@@ -663,7 +662,7 @@ static void ctx_tables(shade_ctx *c) {
                                    &kx, &ky);
     if (cone && c->n_sun > 1 && !(c->f->flags & (VXO_FLAG_NO_DOOM | VXO_FLAG_SOFT_BRICK))) {
         int p[7];
-        vxo_doom_plan((const float(*)[3])c->sun_dirs, c->n_sun, c->max_steps, kx, ky, p);
+        vxo_doom_plan((const float(*)[3])c->sun_dirs, c->n_sun, c->max_steps, p);
         if (p[6] < 1) {
             /* no h can meet the stop rule at this MAX: no table */
         } else if (s->held_doom && !memcmp(p, s->held_dplan, sizeof p)) {
@@ -673,7 +672,6 @@ static void ctx_tables(shade_ctx *c) {
             vxo_field_doom(s->field, s->X, s->Y, s->Z, p, c->doom_owned);
             c->doom = c->doom_owned;
         }
-        c->doom_k2 = 2 * (kx + ky + 1);
     }
     for (int k = 0; k < c->n_sun; k++) {
         if (oct[k] < 0) continue;
@@ -824,14 +822,14 @@ static void shade_frag(const shade_ctx *c, const vxo_gbuf *g, const float ray[3]
     if (shadeFactor > 0.0f && !(f->flags & 0x1u)) {  /* :232; VX_FLAG_NO_SHADOW skips */
         vxo_march_t sun;
         if (c->n_sun <= 1) {
-            march_ex(s, g->cell, g->fract, sunDir, c->max_steps, &sun, c->ex[0], c->doom, c->doom_k2);   /* :233 */
+            march_ex(s, g->cell, g->fract, sunDir, c->max_steps, &sun, c->ex[0], c->doom);   /* :233 */
             shadeFactor = shadeFactor * (sun.step == c->max_steps ? 1.0f : 0.0f);   /* :234 */
             if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
             rec_march(sun.fetches | (sun.step == c->max_steps ? 1 << 16 : 0));
         } else {                 /* ext soft shadows: lit fraction of the sun samples */
             int lit = 0;
             for (int k = 0; k < c->n_sun; k++) {
-                march_ex(s, g->cell, g->fract, c->sun_dirs[k], c->max_steps, &sun, c->ex[k], c->doom, c->doom_k2);
+                march_ex(s, g->cell, g->fract, c->sun_dirs[k], c->max_steps, &sun, c->ex[k], c->doom);
                 lit += sun.step == c->max_steps ? 1 : 0;
                 if (st) { st->shadow_rays++; st->shadow_fetches += (uint64_t)sun.fetches; }
                 rec_march(sun.fetches | (sun.step == c->max_steps ? 1 << 16 : 0));

@@ -31,17 +31,21 @@ def _wmax(D, lo, hi, axis):
     return out
 
 
-def _doom_numpy(field, dirs, max_steps, kx, ky):
+def _doom_numpy(field, dirs, max_steps):
     """Depth recursion over Q x Q sub-cells per cell, top layer down, in the
     sun-aligned grid (x, y mirrored where the sun's component is negative);
-    h up to the largest value the stop rule can use at landing 1."""
+    h up to the largest value the stop rule can use at landing 1; a doomed
+    cell holds its crossing bound C(h)."""
     d = np.asarray(dirs, np.float32).reshape(-1, 3)
-    hmax = min(HCAP, (max_steps - 2) // (2 * (kx + ky + 1)) - 1)
+    hmax = 0
     ax = np.abs(d[:, 0].astype(np.float64) / d[:, 2].astype(np.float64))
     ay = np.abs(d[:, 1].astype(np.float64) / d[:, 2].astype(np.float64))
     xlo, xhi = math.floor(Q * (ax.min() - EPS)), math.ceil(Q * (ax.max() + EPS))
     ylo, yhi = math.floor(Q * (ay.min() - EPS)), math.ceil(Q * (ay.max() + EPS))
     sx, sy = (1 if d[0, 0] > 0 else -1), (1 if d[0, 1] > 0 else -1)
+    cross = lambda h: h + (h * xhi) // Q + 1 + (h * yhi) // Q + 1       # boundary crossings to the block
+    while hmax < HCAP and cross(hmax + 1) <= HCAP and 1 + 2 * cross(hmax + 1) < max_steps:
+        hmax += 1
     solid = (field[..., 0] == 0) & (field[..., 1] == 0)
     if sx < 0:
         solid = solid[:, :, ::-1]
@@ -57,7 +61,8 @@ def _doom_numpy(field, dirs, max_steps, kx, ky):
     for z in range(Z - 1, -1, -1):
         m = _wmax(_wmax(D1, -1, Q + xhi, 1), -1, Q + yhi, 0)[::Q, ::Q]
         h = m.astype(np.int32) + 1
-        code[z] = np.where((m < 255) & (h <= hmax) & ~solid[z], h + 1, 0)
+        cr = np.array([cross(int(v)) if v <= hmax else 0 for v in range(256)], np.int32)
+        code[z] = np.where((m < 255) & (h <= hmax) & ~solid[z], cr[np.minimum(h, 255)], 0)
         s = solid[z]
 
         def cov(cy, cx):
@@ -99,8 +104,8 @@ def test_field_doom_matches_numpy_restatement(field, el, az, radius, n, max_step
     cone, _, kx, ky = oracle.exit_plan(d)
     assert cone
     maxs = max_steps or 2 * field.shape[0]            # render.frag:12 (2 Z), or a frame's own
-    ref, plan = _doom_numpy(field, d, maxs, kx, ky)
-    assert oracle.doom_plan(d, maxs, kx, ky) == plan
+    ref, plan = _doom_numpy(field, d, maxs)
+    assert oracle.doom_plan(d, maxs) == plan
     got = oracle.field_doom(field, plan)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref), int((got != ref).sum())

@@ -483,16 +483,14 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, bool doom, const int 
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
 // a.sunc (cone) built or found, and the info filled.  A soft-shadow frame's
 // cone copy carries the doom table unless the frame asks VX_FLAG_NO_DOOM or
-// VX_FLAG_SOFT_BRICK (the LDS brick march reads no doom codes); doom_k2 = 2 (kx
-// + ky + 1) then, else 0.  The hard shadow's march has no doom rule: on C3 the
+// VX_FLAG_SOFT_BRICK (the LDS brick march reads no doom codes).  The hard shadow's march has no doom rule: on C3 the
 // table saved no time and the rule's per-lane landing count cost +1.7 %
 // (profiles/r06_ab_doom2_c3.txt).
 static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &fc, hipStream_t st,
                       const int8_t **sunc, vx_exit_info *info, bool *built, vx_scene::Cone **used,
-                      int *doom_k2, hipEvent_t t_build = nullptr) {
+                      hipEvent_t t_build = nullptr) {
     *sunc = nullptr;
     *used = nullptr;
-    if (doom_k2) *doom_k2 = 0;
     bool b = false;
     vx_exit_info e{0, -1, -1, -1, 0.0f};
     const bool tables = s->d_sunx && !(p->flags & VX_FLAG_NO_EXIT);
@@ -500,11 +498,10 @@ static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &
         int oct, kx, ky;
         if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
             int plan[7] = {0, 0, 0, 0, 0, 0, 0};
-            doom_plan(fc, kx, ky, plan);
+            doom_plan(fc, plan);
             const bool doom = fc.n_sun > 1 && plan[6] >= 1 && !(p->flags & (VX_FLAG_NO_DOOM | VX_FLAG_SOFT_BRICK));
             const int rc = cone_copy(s, oct, kx, ky, doom, plan, st, sunc, &b, used, t_build);
             if (rc) return rc;
-            if (doom && doom_k2) *doom_k2 = 2 * (kx + ky + 1);
             e = vx_exit_info{2, oct, kx, ky, 0.0f};
         } else if (fc.sun_k[0].fast) {
             const float *r = fc.sun_k[0].r;
@@ -566,7 +563,7 @@ static int do_render(vx_scene *s, const vx_frame_params *p, int w, int h, const 
     std::unique_lock<std::mutex> cone_lock(s->cone_mu);
     vx_scene::Cone *cone = nullptr;
     {
-        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone, &a.doom_k2);
+        const int rc = frame_exit(s, p, a.fc, st, &a.sunc, nullptr, nullptr, &cone);
         if (rc) return rc;
     }
     if (!cone) cone_lock.unlock();
@@ -645,7 +642,7 @@ int vx_prepare_sun(vx_scene *s, const vx_frame_params *p, void *stream, vx_exit_
         // ev0 is recorded inside cone_copy right before the build's first packet:
         // build_ms is the copy's GPU time, not the host's allocation or waits
         std::lock_guard<std::mutex> lock(s->cone_mu);
-        rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, nullptr, s->ev0);
+        rc = frame_exit(s, p, fc, st, &sunc, info, &built, &cone, s->ev0);
         if (rc) return rc;
         if (built) VX_HIP(hipEventRecord(s->ev1, st));
     }

@@ -183,7 +183,7 @@ int exit_plan(const FrameConsts &fc, int SB, int *oct, int *kx, int *ky) {
 
 // vx_internal.h doom_plan; the oracle's vxo_doom_plan restated (same double
 // arithmetic on the same fp32 directions)
-void doom_plan(const FrameConsts &fc, int kx, int ky, int plan[7]) {
+void doom_plan(const FrameConsts &fc, int plan[7]) {
     double axmin = 1e300, axmax = -1e300, aymin = 1e300, aymax = -1e300;
     for (int k = 0; k < fc.n_sun; k++) {
         const float *r = fc.sun_k[k].r;
@@ -196,7 +196,10 @@ void doom_plan(const FrameConsts &fc, int kx, int ky, int plan[7]) {
     plan[1] = fc.sun_k[0].r[1] > 0.0f ? 1 : -1;
     plan[2] = (int)std::floor(Q * (axmin - eps)); plan[3] = (int)std::ceil(Q * (axmax + eps));
     plan[4] = (int)std::floor(Q * (aymin - eps)); plan[5] = (int)std::ceil(Q * (aymax + eps));
-    const int dk2 = 2 * (kx + ky + 1), hm = fc.max_steps >= 2 ? (fc.max_steps - 2) / dk2 - 1 : -1;
-    plan[6] = hm < kDoomHCap ? hm : kDoomHCap;
+    int hm = 0;
+    while (hm < kDoomHCap && doom_cross(hm + 1, plan[3], plan[5]) <= kDoomHCap &&
+           1 + 2 * doom_cross(hm + 1, plan[3], plan[5]) < fc.max_steps)
+        hm++;
+    plan[6] = hm;
 }
 }  // namespace vx

@@ -80,7 +80,6 @@ struct KernelArgs {
     unsigned SXpYp, sunp_texels;
     const int8_t *sunx;      // 8 orthant-exit copies of sunp's channel, one per ray octant (bit i: r_i > 0), or nullptr
     const int8_t *sunc;      // the frame's cone-exit copy (every sample of the frame reads it), or nullptr
-    int doom_k2;             // > 0: sunc carries doom codes (launch_sun_doom), 2 (kx + ky + 1) of its window
     const uint16_t *rg;      // R | G << 8 per cell
     const uint32_t *rg2;     // AO x-pairs (X + 1 per row): entry p = (R, G) of cells clamp(p - 1), clamp(p)
     const uint32_t *noise;   // RGBA8 noise texels
@@ -170,8 +169,9 @@ int launch_sun_cone(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
 // cone copy already holding its exit marks and face bits, every cell from which
 // every ray of the sub-cell window {sx, sy, xlo, xhi, ylo, yhi} (doom_plan)
 // provably enters a solid cell h <= hmax layers up, and whose march texel is
-// >= 1, becomes kDoomBase - h (-9 .. -128); the march reads the texel itself
-// from the plain channel when it goes on from such a cell.
+// >= 1, becomes kDoomBase - doom_cross(h) (-9 .. -128, doom_cross <= kDoomHCap): the boundary crossings
+// a march makes from it into the block; the march reads the texel itself from
+// the plain channel when it goes on from such a cell.
 constexpr int kDoomQ = 8, kDoomHCap = 120, kDoomBase = -8;
 // the stop rule's soundness: a march step ends within 0.1024 cell of where its
 // segment entered the doomed ray's solid region (T = 1, |r_a| >= 2^-10), inside
@@ -179,10 +179,15 @@ constexpr int kDoomQ = 8, kDoomHCap = 120, kDoomBase = -8;
 static_assert(kDoomQ <= 9, "doom margin 1/Q must exceed the 0.1024-cell step overshoot plus drift");
 int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int SB, const int plan[7], void *stream);
 // the doom table's plan for a frame's samples (all fast, one octant, r_z > 0)
-// and cone window kx, ky (oracle vxo_doom_plan): sx, sy, the per-layer
-// sub-cell offsets xlo, xhi, ylo, yhi, and hmax, the largest h whose stop rule
-// j + (h + 1) 2 (kx + ky + 1) < MAX_STEPS can hold (hmax < 1: no table)
-void doom_plan(const FrameConsts &fc, int kx, int ky, int plan[7]);
+// (oracle vxo_doom_plan): sx, sy, the per-layer sub-cell offsets xlo, xhi,
+// ylo, yhi, and hmax, the largest h whose stop rule j + 2 doom_cross(h) <
+// MAX_STEPS can hold (hmax < 1: no table)
+void doom_plan(const FrameConsts &fc, int plan[7]);
+// crossings from a doomed cell with h into its block (oracle vxo_doom_cross):
+// h in z, floor(h xhi / Q) + 1 in x, floor(h yhi / Q) + 1 in y
+constexpr int doom_cross(int h, int xhi, int yhi) {   // (constexpr: host and device)
+    return h + (h * xhi) / kDoomQ + 1 + (h * yhi) / kDoomQ + 1;
+}
 // which copy a frame's sun march reads: 1 = one cone copy {oct, kx, ky} for every
 // sample (all on the fast path, one sign pattern, r_z > 0, slopes <= 4, kx, ky
 // <= SB); 0 = each fast sample its octant's orthant copy (oracle vxo_exit_plan)

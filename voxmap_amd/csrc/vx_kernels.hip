@@ -501,7 +501,7 @@ __global__ void k_sun_cone_layer(const int8_t *ch, int8_t *out, int X, int Y, in
 // xlo, gx + xhi], xlo >= -1) in LDS, takes the window maxima separably (rows
 // per wave; a cell's wide row window split over 8 lanes and joined by lane
 // shuffles), writes d0 and turns each doomed cell (h <= hmax) of the cone copy
-// whose march texel is >= 1 into kDoomBase - h.  Solid = R = G = 0
+// whose march texel is >= 1 into kDoomBase - doom_cross(h).  Solid = R = G = 0
 // (sdf.cpp:430) inside the grid.  No integer division: every loop walks rows
 // by wave and columns by lane.
 // xhi <= ceil(Q (4 + 1/64)) = 4 Q + 1 (cone plans: |r_x / r_z| <= 4)
@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t n
             for (int r = kDoomQ * j; r <= kDoomQ * j + kDoomQ + 1 + yhi; r++) m = max(m, (int)s_rc[r][i]);
             if (m < 255 && m + 1 <= hmax) {
                 const size_t p = real(xa, ya);
-                if (sunc[p] >= 1) sunc[p] = (int8_t)(kDoomBase - (m + 1));
+                if (sunc[p] >= 1) sunc[p] = (int8_t)(kDoomBase - doom_cross(m + 1, xhi, yhi));
             }
         }
     }
@@ -767,7 +767,7 @@ int launch_sun_doom(const int8_t *sunp, int8_t *sunc, int X, int Y, int Z, int S
     const int sx = plan[0], sy = plan[1], xlo = plan[2], xhi = plan[3], ylo = plan[4], yhi = plan[5], hmax = plan[6];
     // the block's staged window (k_doom_layer): xlo, ylo >= -1, xhi, yhi <= kDoomXhi; codes down to -128
     if (xlo < -1 || ylo < -1 || xhi > kDoomXhi || yhi > kDoomXhi || xlo > xhi || ylo > yhi || SB < 1 || hmax < 1 ||
-        hmax > kDoomHCap)
+        hmax > kDoomHCap || doom_cross(hmax, xhi, yhi) > 120)
         return (int)hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     const int SXp = X + 2 * SB, SYp = Y + 2 * SB, SZp = Z + 2 * SB;

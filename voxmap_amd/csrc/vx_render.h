@@ -421,16 +421,16 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
 // offset terms, len = the first step's length (march_len_sg), rsrc = the
 // channel's typed-load descriptor (march_pad; march_soft shares these across
 // the samples of a fragment).
-// A doom code (soft-shadow frames' cone copies, launch_sun_doom: kDoomBase - h)
+// A doom code (soft-shadow frames' cone copies, launch_sun_doom: kDoomBase - C)
 // read at landing j: the cell is one from which every ray of the frame's window
-// meets a solid cell h layers up, so the march lands on a 0 texel within (h +
-// 1) 2 (kx + ky + 1) landings -- unlit (0) if that is before MAX_STEPS, else
+// meets a solid cell after at most C boundary crossings, so the march lands on
+// a 0 texel within 2 C landings -- unlit (0) if that is before MAX_STEPS, else
 // the march goes on from the cell's texel T, read from the plain channel
 // (oracle march_ex).  Anything else is returned as read.
 __device__ __forceinline__ float doom_resolve(const KernelArgs &a, float t, int j, int maxs, unsigned off) {
     if (t <= -8.5f) {
-        const int d = (int)(-7.0f - t);                                           // h + 1
-        t = j + d * a.doom_k2 < maxs ? 0.0f : ld_fmt1(buf_rsrc(a.sunp - 0x4B000000, kRsrcS8), off);
+        const int c = (int)(-8.0f - t);                                           // C
+        t = j + 2 * c < maxs ? 0.0f : ld_fmt1(buf_rsrc(a.sunp - 0x4B000000, kRsrcS8), off);
     }
     return t;
 }
