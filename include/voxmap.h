@@ -34,7 +34,7 @@ extern "C" {
  * canvas byte with clamped source and alpha (render.js:84-86, map.js:7), band /
  * tile lists are cached per distinct list, no caller stream handle is kept,
  * a zeroed dist_cap falls back to VX_FALLBACK_DIST_CAP where 64 does not fit,
- * and soft-shadow frames read the sun doom table (VX_FLAG_NO_DOOM: without). */
+ * and the sun march reads the doom table (VX_FLAG_NO_DOOM: without). */
 #define VX_ABI_VERSION 10
 
 /* error codes */

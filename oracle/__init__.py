@@ -115,7 +115,7 @@ class Oracle:
         them -- fields with Z <= 126 and every R, G <= Z (its padded int8 march
         copies) -- so the shadow fetch counters match the kernel's;
         exit="orthant": the orthant tables only (the kernel's VX_FLAG_NO_CONE).
-        With a cone table a soft-shadow frame also reads the sun doom table
+        With a cone table a frame also reads the sun doom table
         (vxo_field_doom) unless its flags carry VX_FLAG_NO_DOOM or VX_FLAG_SOFT_BRICK.
         Frames are identical in every mode.
 
@@ -165,7 +165,7 @@ class Oracle:
         self._held = field_exit(self.field, octs[0], kx, ky)
         self.sc.held = self._held.ctypes.data
         self.sc.held_oct, self.sc.held_kx, self.sc.held_ky = octs[0], kx, ky
-        if cone and len(d) > 1 and not (params.flags & (0x20000 | 0x100)):   # soft shadows: the doom table
+        if cone and not (params.flags & (0x20000 | 0x100)):      # the cone plan's doom table
             Z = self.sc.Z
             plan = doom_plan(d, params.max_shadow_steps if params.max_shadow_steps > 0 else 2 * Z)
             if plan[6] >= 1:

@@ -98,8 +98,7 @@ typedef struct {
  * the GL blend stage (blend_canvas) changes.  Not a kernel flag. */
 #define VXO_FLAG_BLEND_FLOAT 0x10000u
 /* The sun doom table (DESIGN.md §3 "Doom table"), restated from the kernel's
- * launch_sun_doom: where a soft-shadow frame (shadow_samples >= 2) reads a
- * cone exit copy, a cell from which every ray of the frame's sun samples
+ * launch_sun_doom: where a frame reads a cone exit copy, a cell from which every ray of the frame's sun samples
  * provably enters a solid cell h layers up (h <= the plan's hmax) ends the
  * march unlit at once when the march lands there early enough (landing index
  * j with j + 2 C < MAX, C = vxo_doom_cross(h)); later, the march goes on with

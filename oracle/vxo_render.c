@@ -660,7 +660,7 @@ static void ctx_tables(shade_ctx *c) {
     /* the kernel's cone copies need Z >= 3 (their window inside its -1 border) */
     const int cone = vxo_exit_plan((const float(*)[3])c->sun_dirs, c->n_sun, s->exit_mode == 1 && s->Z >= 3, oct,
                                    &kx, &ky);
-    if (cone && c->n_sun > 1 && !(c->f->flags & (VXO_FLAG_NO_DOOM | VXO_FLAG_SOFT_BRICK))) {
+    if (cone && !(c->f->flags & (VXO_FLAG_NO_DOOM | VXO_FLAG_SOFT_BRICK))) {
         int p[7];
         vxo_doom_plan((const float(*)[3])c->sun_dirs, c->n_sun, c->max_steps, p);
         if (p[6] < 1) {

@@ -84,9 +84,9 @@ def _sun(el_deg, az_deg):
 
 
 # every sign pattern of (r_x, r_y) with r_z > 0, steep to low (slopes up to 4)
-# (soft-shadow frames read the table: radius, samples)
+# (radius, samples): hard and soft shadows
 SUNS = [(33, 30, 0.02, 4), (40, 120, 0.02, 4), (60, 210, 0.03, 8), (20, 300, 0.02, 2), (15, 45, 0.01, 4),
-        (45, 160, 0.05, 8)]
+        (45, 160, 0.05, 8), (33, 30, 0.0, 1), (15, 45, 0.0, 1)]
 
 
 @pytest.fixture(scope="module")
@@ -142,9 +142,9 @@ def test_doom_frames_identical_with_fewer_fetches(field, noise):
             ib, sb = o.render(fb.params, 96, 64)
             assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32)), (maxs, el, az)
             assert sa.as_dict()["shadow_fetches"] <= sb.as_dict()["shadow_fetches"]
-    # the hard shadow has no doom rule: a one-sample frame counts the same fetches either way
+    # the hard shadow reads the table too: a one-sample frame saves fetches
     a = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(15, 45), flags=vx.FLAG_FULL_QUALITY)
     b = vx.make_frame((48.0, 32.0, 36.0), (1.1, 0.0, 0.5), 96, 64, sun=_sun(15, 45),
                       flags=vx.FLAG_FULL_QUALITY | NO_DOOM)
-    assert o.render(a.params, 96, 64)[1].as_dict()["shadow_fetches"] == \
+    assert o.render(a.params, 96, 64)[1].as_dict()["shadow_fetches"] < \
         o.render(b.params, 96, 64)[1].as_dict()["shadow_fetches"]

@@ -7,7 +7,7 @@ with and without the table (so the device table and the march's stopping rule
 agree with vxo_field_doom and march_ex landing by landing in count); at the
 bench scenes (S-proc, S-glass, C5's 3^3 field) with C5's 16 soft samples frames
 are identical with and without the table and the table removes shadow fetches.
-Only soft-shadow frames read the table."""
+Hard and soft shadows read the table."""
 import math
 
 import numpy as np
@@ -35,7 +35,7 @@ def _sun(el_deg, az_deg):
     return (math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el))
 
 
-# soft-shadow frames read the table (the hard shadow's march has no doom rule): one hard sun too
+# soft shadows, and hard shadows (one sample)
 SUNS = [(33, 30, 0.02, 4), (40, 120, 0.02, 4), (60, 210, 0.03, 8), (20, 300, 0.02, 2), (15, 45, 0.01, 4),
         (45, 160, 0.05, 8), (25, 250, 0.04, 16), (15, 45, 0.0, 1)]
 

@@ -45,15 +45,18 @@ def test_product_kernels_spill_limits(meta):
 
 
 def test_no_spill_inside_a_step_loop(built):
-    """No RGBA8 render kernel (every EXT mode) holds a spill instruction inside
-    a march or primary step loop (kernel_meta.hot_loop_spills); the rare paths
-    (glass in draw order where panes stack) may spill, outside them."""
+    """No RGBA8 render kernel (every EXT mode) holds more spill instructions
+    inside a march or primary step loop (kernel_meta.hot_loop_spills) than its
+    mode allows: none, except the few reloads the doom rule's step loop takes
+    in EXT 1/2/5 (kernel_meta.HOT_LOOP_SPILL_LIMITS, measured faster than the
+    spill-free form); the rare paths (glass in draw order where panes stack)
+    may spill, outside them."""
     from voxmap_amd import build as vb
     from voxmap_amd import kernel_meta
     hot = kernel_meta.hot_loop_spills(vb.OUT)
     assert len(hot) == 24, sorted(hot)
     for p, (loops, n) in hot.items():
-        assert loops > 0 and n == 0, (p, loops, n)
+        assert loops > 0 and n <= kernel_meta.HOT_LOOP_SPILL_LIMITS.get(p[3], 0), (p, loops, n)
 
 
 def test_v1_kernel_main_path_spill_free(meta):

@@ -481,11 +481,9 @@ static int cone_copy(vx_scene *s, int oct, int kx, int ky, bool doom, const int 
 }
 
 // The sun exit copy frame constants fc select (vx_exit_info kind 0/1/2):
-// a.sunc (cone) built or found, and the info filled.  A soft-shadow frame's
-// cone copy carries the doom table unless the frame asks VX_FLAG_NO_DOOM or
-// VX_FLAG_SOFT_BRICK (the LDS brick march reads no doom codes).  The hard shadow's march has no doom rule: on C3 the
-// table saved no time and the rule's per-lane landing count cost +1.7 %
-// (profiles/r06_ab_doom2_c3.txt).
+// a.sunc (cone) built or found, and the info filled.  A frame's cone copy
+// carries the doom table unless the frame asks VX_FLAG_NO_DOOM or
+// VX_FLAG_SOFT_BRICK (the LDS brick march reads no doom codes).
 static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &fc, hipStream_t st,
                       const int8_t **sunc, vx_exit_info *info, bool *built, vx_scene::Cone **used,
                       hipEvent_t t_build = nullptr) {
@@ -499,7 +497,7 @@ static int frame_exit(vx_scene *s, const vx_frame_params *p, const FrameConsts &
         if (!(p->flags & VX_FLAG_NO_CONE) && exit_plan(fc, s->SB, &oct, &kx, &ky)) {
             int plan[7] = {0, 0, 0, 0, 0, 0, 0};
             doom_plan(fc, plan);
-            const bool doom = fc.n_sun > 1 && plan[6] >= 1 && !(p->flags & (VX_FLAG_NO_DOOM | VX_FLAG_SOFT_BRICK));
+            const bool doom = plan[6] >= 1 && !(p->flags & (VX_FLAG_NO_DOOM | VX_FLAG_SOFT_BRICK));
             const int rc = cone_copy(s, oct, kx, ky, doom, plan, st, sunc, &b, used, t_build);
             if (rc) return rc;
             e = vx_exit_info{2, oct, kx, ky, 0.0f};

@@ -421,7 +421,7 @@ __device__ __forceinline__ bool march_fast(const KernelArgs &a, const SunRay &S,
 // offset terms, len = the first step's length (march_len_sg), rsrc = the
 // channel's typed-load descriptor (march_pad; march_soft shares these across
 // the samples of a fragment).
-// A doom code (soft-shadow frames' cone copies, launch_sun_doom: kDoomBase - C)
+// A doom code (a frame's cone copy, launch_sun_doom: kDoomBase - C)
 // read at landing j: the cell is one from which every ray of the frame's window
 // meets a solid cell after at most C boundary crossings, so the march lands on
 // a 0 texel within 2 C landings -- unlit (0) if that is before MAX_STEPS, else
@@ -435,11 +435,15 @@ __device__ __forceinline__ float doom_resolve(const KernelArgs &a, float t, int 
     return t;
 }
 
-// DOOM: the copy may hold doom codes.  The peeled first landing resolves its
-// own; a code read in the loop ends the loop like any negative value and is
-// resolved after it (landing step + 1), a late one marching on in a per-lane
-// loop of its own, so the main loop keeps its scalar step count.
-template <int SG, bool DOOM = false>
+// DOOM (kDoomAfter): the copy may hold doom codes.  The peeled first landing
+// resolves its own; a code read in the loop ends the loop like any negative
+// value and is resolved after it (landing j), a late one marching on in a
+// per-lane loop of its own, so the main loop keeps its scalar step count.
+// (Resolving in the loop at the wave's landing instead measured slower on C5
+// and C3, though it keeps the hard units' step loop free of spills:
+// profiles/r06_ab_doom3_c5.txt, r06_ab_doom10_*.txt.)
+constexpr int kDoomNone = 0, kDoomAfter = 1;
+template <int SG, int DOOM = kDoomNone>
 __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay &S, u32x4 rsrc, float exy, float e2,
                                                float len, float f0, float f1, float f2, Counters &cnt) {
     const float r0 = S.r[0], r1 = S.r[1], r2 = S.r[2];
@@ -466,7 +470,7 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
         float t = ld_fmt1(rsrc, advance());                                        // :123-128
         len = march_len_sg<SG>(S, f0, f1, f2);  // next step, under the load
         cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
-        if constexpr (DOOM) t = doom_resolve(a, t, 1, maxs, cell_off());
+        if constexpr (DOOM != kDoomNone) t = doom_resolve(a, t, 1, maxs, cell_off());
         tv = t;
         cnt.march_witers += once_per_wave(1u);
         cnt.march_slots += once_per_wave(nl);
@@ -479,11 +483,11 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
             len = march_len_fract<SG>(S, f0, f1, f2);   // next step, under the load
             cnt.shadow_fetch += t >= 0.0f ? 1u : 0u;
             tv = t;
-            if constexpr (DOOM) ++j;
+            if constexpr (DOOM == kDoomAfter) ++j;
             cnt.march_witers += once_per_wave(1u);   // counted in the loop: step stays a scalar
             cnt.march_slots += once_per_wave(nl);
         } while (tv > 0.0f && ++step < maxs - 1);
-        if constexpr (DOOM) {
+        if constexpr (DOOM == kDoomAfter) {
             if (tv <= -8.5f) {                 // a doom code at landing j
                 tv = doom_resolve(a, tv, j, maxs, cell_off());
                 while (tv > 0.0f && j < maxs - 1) {   // late: on from the cell's texel (rare)
@@ -505,7 +509,7 @@ __device__ __forceinline__ bool march_pad_from(const KernelArgs &a, const SunRay
     return tv != 0.0f;
 }
 
-template <int SG, bool DOOM = false>   // the sun's axis signs (bit i: r_i > 0); DOOM: see march_pad_from
+template <int SG, int DOOM = kDoomNone>   // the sun's axis signs (bit i: r_i > 0); DOOM: see march_pad_from
 __device__ __forceinline__ bool march_pad(const KernelArgs &a, const SunRay &S, const int8_t *sun, float c0, float c1,
                                           float c2, float f0, float f1, float f2, Counters &cnt) {
     const float xpf = (float)a.SXp;
@@ -536,7 +540,7 @@ __device__ __forceinline__ int march_soft(const KernelArgs &a, const int8_t *sun
     for (int k = 0; k < F.n_sun; k++) {
         cnt.shadow_rays++;
         const SunRay S = F.sun_k[k];
-        lit += march_pad_from<SG, true>(a, S, rsrc, exy, e2, march_len_d(S, d0, d1, d2), f0, f1, f2, cnt) ? 1 : 0;
+        lit += march_pad_from<SG, kDoomAfter>(a, S, rsrc, exy, e2, march_len_d(S, d0, d1, d2), f0, f1, f2, cnt) ? 1 : 0;
     }
     return lit;
 }
@@ -680,6 +684,9 @@ __device__ __forceinline__ bool first_step_exit(const KernelArgs &a, const int8_
 // S by value: the soft-shadow loop indexes sun_k[k] dynamically, and a
 // reference into the kernel argument there made the compiler copy the whole
 // KernelArgs (1.5 KB) to scratch.
+// (the per-sample soft loop runs only where no cone copy serves every sample,
+// so it never reads a doom code; it keeps the same form, which measured faster)
+template <int DOOM = kDoomAfter>
 __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, float c0, float c1, float c2, float f0,
                                           float f1, float f2, Counters &cnt) {
     if (S.fast && a.sunp) {
@@ -689,9 +696,10 @@ __device__ __forceinline__ bool march_sun(const KernelArgs &a, const SunRay S, f
         const int8_t *ch = a.sunc ? a.sunc
                          : a.sunx ? a.sunx + (size_t)sg * a.sunp_texels : S.up ? a.sunp : a.sunp + a.sunp_texels;
         switch (sg) {
-#define VX_SG(K) case K: return march_pad<K>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
+        // (DOOM: the frame's cone copy may hold doom codes, launch_sun_doom)
+#define VX_SG(K) case K: return march_pad<K, DOOM>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
             VX_SG(0) VX_SG(1) VX_SG(2) VX_SG(3) VX_SG(4) VX_SG(5) VX_SG(6)
-            default: return march_pad<7>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
+            default: return march_pad<7, DOOM>(a, S, ch, c0, c1, c2, f0, f1, f2, cnt);
 #undef VX_SG
         }
     }
@@ -1897,10 +1905,10 @@ void k_render(KernelArgs a) {
                             }
                         } else {
                             switch (sgv) {
-#define VX_SGP(K) case K: lit = march_pad<K, true>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
+#define VX_SGP(K) case K: lit = march_pad<K, kDoomAfter>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z, \
                                                    cnt); break;
                                 VX_SGP(0) VX_SGP(1) VX_SGP(2) VX_SGP(3) VX_SGP(4) VX_SGP(5) VX_SGP(6)
-                                default: lit = march_pad<7, true>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
+                                default: lit = march_pad<7, kDoomAfter>(a, S, ch, pc.x, pc.y, pc.z, pf.x, pf.y, pf.z,
                                                                   cnt);
 #undef VX_SGP
                             }

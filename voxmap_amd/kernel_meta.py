@@ -31,6 +31,11 @@ STATS_SCRATCH_LIMIT = 512       # the counting (STATS) instantiations keep ~16 c
 # (round 6, ADVICE r05: EXT 0 17, EXT 1 58, EXT 2 60, EXT 3 65, EXT 4 115,
 # EXT 5 13, EXT 6 14 slots, all in tiled instantiations): a change that moves
 # one is a change to look at, and the limit moves with it, measured.
+# round 6: the sun march with the doom rule (its codes resolved after the
+# step loop) reloads a few SGPR / scratch values inside the hard units' step
+# loop; measured faster than the spill-free in-loop form on C3, v1 and
+# REFLECT_ALL (profiles/r06_ab_doom10_c3.txt), so a handful is allowed there
+HOT_LOOP_SPILL_LIMITS = {1: 8, 2: 2, 5: 8}
 SPILL_LIMITS = {0: 19, 1: 62, 2: 64, 3: 70, 4: 132, 5: 16, 6: 16}
 V1_SCRATCH_LIMIT = 72           # EXT 0's private segment (64 B now): the chain's slots, no KernelArgs copy
 RENDER_VGPR_LIMIT = 64          # 8 waves/SIMD
@@ -183,7 +188,7 @@ def check(lib: str) -> dict[str, dict[str, int]]:
     for p, (loops, n) in hot_loop_spills(lib).items():
         if not loops:
             bad.append(f"k_render{p}: no march / primary loop found in the disassembly (check the parser)")
-        if n:
+        if n > HOT_LOOP_SPILL_LIMITS.get(p[3] if p else -1, 0):
             bad.append(f"k_render{p}: {n} spill instructions inside a march / primary loop")
     if bad:
         raise RuntimeError("render kernel resource check failed:\n  " + "\n  ".join(bad))
