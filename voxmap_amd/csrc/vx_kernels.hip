@@ -561,13 +561,27 @@ __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t n
     __syncthreads();
     // rows: lane c the state window [c + 1 + xlo, c + 1 + xhi]; the cells' windows
     // [Q i, Q i + Q + 1 + xhi] as 8 lanes per cell (lane = 8 i + p reads Q i + p + 8 k)
+    // (windows of up to 4 taps, and the cells' strided reads, as fixed unrolled
+    // loops with a wave-uniform bound: no per-tap loop control)
     const int ci = lane >> 3, cp = lane & 7, chi = kDoomQ * ci + kDoomQ + 1 + xhi;
+    const int wx = xhi - xlo + 1, wy = yhi - ylo + 1;
+    constexpr int kCellTaps = (kDoomQ + 2 + kDoomXhi + 7) / 8;
     for (int r = wv; r < H; r += 4) {
         int m = 0;
-        for (int q = lane + 1 + xlo; q <= lane + 1 + xhi; q++) m = max(m, (int)s_d[r][q]);
+        if (wx <= 4) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (k < wx) m = max(m, (int)s_d[r][lane + 1 + xlo + k]);
+        } else {
+            for (int q = lane + 1 + xlo; q <= lane + 1 + xhi; q++) m = max(m, (int)s_d[r][q]);
+        }
         s_rx[r][lane] = (uint8_t)m;
         int mc = 0;
-        for (int q = kDoomQ * ci + cp; q <= chi; q += 8) mc = max(mc, (int)s_d[r][q]);
+#pragma unroll
+        for (int k = 0; k < kCellTaps; k++) {
+            const int q = kDoomQ * ci + cp + 8 * k;
+            if (q <= chi) mc = max(mc, (int)s_d[r][q]);
+        }
         mc = max(mc, __shfl_xor(mc, 1));
         mc = max(mc, __shfl_xor(mc, 2));
         mc = max(mc, __shfl_xor(mc, 4));
@@ -582,7 +596,13 @@ __global__ void __launch_bounds__(256) k_doom_layer(const int8_t *sunp, size_t n
             const int gy = H0 + j;
             if (gx >= GX || gy >= GY) continue;
             int m = 0;
-            for (int r = j + 1 + ylo; r <= j + 1 + yhi; r++) m = max(m, (int)s_rx[r][i]);
+            if (wy <= 4) {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (k < wy) m = max(m, (int)s_rx[j + 1 + ylo + k][i]);
+            } else {
+                for (int r = j + 1 + ylo; r <= j + 1 + yhi; r++) m = max(m, (int)s_rx[r][i]);
+            }
             const int cj = j >> 3, b = j & 7;
             const int ya0 = cj + 1 - (b == 0 ? 1 : 0), ya1 = cj + 1 + (b == kDoomQ - 1 ? 1 : 0);
             const bool es = s_solid[ya0][xa0] && s_solid[ya0][xa1] && s_solid[ya1][xa0] && s_solid[ya1][xa1];
