@@ -1,7 +1,7 @@
 """Stress of the sun doom table's stop rule (DESIGN.md §3 "Doom table") on the
 oracle: adversarial scenes (sparse random voxels, one-cell-thick floating
 roofs and poles, lattices) over ground, random suns (elevation 14-85 deg, every
-azimuth), 2-16 soft samples, radii 0.005-0.06, default and short step budgets,
+azimuth), hard shadows and 2-16 soft samples, radii 0.005-0.06, default and short step budgets,
 random cameras; every frame with the table must equal the frame without it
 (VX_FLAG_NO_DOOM) word for word.  CPU only (test infrastructure).
 usage: python tools/doom_stress.py SEED SCENES"""
@@ -41,7 +41,7 @@ for it in range(int(sys.argv[2]) if len(sys.argv) > 2 else 6):
         el = rng.uniform(14, 85); az = rng.uniform(0, 360)
         er, ar = math.radians(el), math.radians(az)
         sun = (math.cos(er) * math.cos(ar), math.cos(er) * math.sin(ar), math.sin(er))
-        n = int(rng.choice([2, 4, 8, 16])); rad = rng.uniform(0.005, 0.06)
+        n = int(rng.choice([1, 1, 2, 4, 8, 16])); rad = rng.uniform(0.005, 0.06) if n > 1 else 0.0
         maxs = int(rng.choice([0, 0, 20, 40]))
         cam = (rng.uniform(10, 86), rng.uniform(10, 54), rng.uniform(20, 39))
         rot = (rng.uniform(0.6, 1.4), 0.0, rng.uniform(-3, 3))
