@@ -4,7 +4,7 @@ roofs and poles, lattices) over ground, random suns (elevation 14-85 deg, every
 azimuth), hard shadows and 2-16 soft samples, radii 0.005-0.06, default and short step budgets,
 random cameras; every frame with the table must equal the frame without it
 (VX_FLAG_NO_DOOM) word for word.  CPU only (test infrastructure).
-usage: python tools/doom_stress.py SEED SCENES"""
+usage: python tools/doom_stress.py SEED SCENES [Z (default 40)]"""
 import os
 import sys, math, time
 import numpy as np
@@ -18,7 +18,7 @@ NO_DOOM = 0x20000
 bad = 0; tot = 0; saved = 0; allf = 0
 t0 = time.time()
 for it in range(int(sys.argv[2]) if len(sys.argv) > 2 else 6):
-    X, Y, Z = 96, 64, 40
+    X, Y, Z = 96, 64, int(sys.argv[3]) if len(sys.argv) > 3 else 40
     g = np.zeros((Z, Y, X), np.uint8)
     kind = it % 3
     if kind == 0:    # sparse random voxels
